@@ -1,0 +1,38 @@
+# Build libpech_crc32c.so (gfx950 HIP kernels + C-ABI) in-tree, and the
+# test-only oracle libraries.  `make` is what __graft_entry__.build() runs.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
+SRC = pech_amd/csrc/crc32c_kernels.hip pech_amd/csrc/crc32c_api.cpp
+HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h include/crc32c.h include/pech_crc32c.h
+LIB = pech_amd/libpech_crc32c.so
+OBJ = build/crc32c_kernels.o build/crc32c_api.o
+
+all: $(LIB) oracle
+
+build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build/crc32c_api.o: pech_amd/csrc/crc32c_api.cpp $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
+
+# device assembly for inspection (build/crc32c_kernels-hip-amdgcn-amd-amdhsa-gfx950.s)
+asm: pech_amd/csrc/crc32c_kernels.hip $(HDR)
+	@mkdir -p build
+	cd build && $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -Rpass-analysis=kernel-resource-usage \
+		../pech_amd/csrc/crc32c_kernels.hip -o crc32c_kernels.s
+
+oracle:
+	$(MAKE) -C oracle all
+	@if [ -d /root/reference/include ]; then $(MAKE) -C oracle ref; fi
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all asm oracle clean

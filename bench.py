@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py -- CRC32C GiB/s on device-resident object buffers (BASELINE.json).
+
+One "step" = one pass of the hot path (plan + main kernel of
+libpech_crc32c.so) over one batch of device-resident synthetic buffers.
+Default workload = BASELINE config 3 / per-GPU shard of config 5:
+256 x 4 MiB buffers (1 GiB) per GPU, rotating between 2 distinct batches
+(2 GiB resident) so the 256 MiB Infinity Cache cannot serve a step.
+
+    python bench.py                       # N=1, defaults
+    python bench.py --config c2           # 65,536 x 4 KiB (parity-sized line)
+    torchrun --nproc-per-node N bench.py --gpus N   # one process per GPU
+
+Multi-GPU: batches are independent, so each rank checksums its own shard
+(weak scaling); no collective touches the data path -- the only
+communication is the timing barrier and a MAX all-reduce of the elapsed time.
+
+Prints ONE JSON line (rank 0).  `roofline` is for the main kernel: HIP
+events around every main-kernel launch on the stream it runs on give the
+average launch duration; achieved = algorithmic bytes per launch (sum of
+buffer lengths) / that duration, against 8.0 TB/s HBM3E peak
+(/opt/skills/guides/MI355X_MICROARCH.md).  `cpu_baseline` times the
+reference crc32c() (oracle/_ref, compiled from the reference header) on
+rank 0's host cores over a bounded sample of the same buffers, and checks
+the GPU outputs for that sample bit-exact.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (list of buffer sizes per GPU, rotate, description)
+    "c2": ([4096] * 65536, 4, "c2: 65,536 x 4 KiB device-resident buffers per GPU, 4 rotating batches (1 GiB)"),
+    "c3": ([4 << 20] * 256, 2, "c3: 256 x 4 MiB device-resident buffers per GPU, 2 rotating batches (2 GiB)"),
+    "c4": (None, 2, "c4: mixed 4 KiB/64 KiB/1 MiB/4 MiB, equal bytes per class (1 GiB) per GPU, shuffled seed 42, "
+                    "2 rotating batches"),
+}
+
+
+def c4_sizes():
+    rng = np.random.default_rng(42)
+    sizes = [4096] * 65536 + [65536] * 4096 + [1 << 20] * 256 + [4 << 20] * 64
+    rng.shuffle(sizes)
+    return sizes
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import pech_amd as P
+    from pech_amd import _lib
+
+    sizes, rotate, desc = CONFIGS[args.config]
+    if sizes is None:
+        sizes = c4_sizes()
+    sizes = np.asarray(sizes, dtype=np.int64)
+    n = len(sizes)
+    batch_bytes = int(sizes.sum())
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+
+    # resident inputs: `rotate` distinct batches of random bytes + descriptors
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    bufs, descs = [], []
+    for r in range(rotate):
+        b = torch.randint(0, 256, (batch_bytes,), dtype=torch.uint8, device=dev, generator=gen)
+        bufs.append(b)
+        descs.append(P.make_descs(b.data_ptr() + offs, sizes, device=dev))
+    outs = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(rotate)]
+    assert _lib.lib().crc32c_dev_reserve(n) == 0
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i):
+        P.dev_batch_async(descs[i % rotate], outs[i % rotate], stream=stream)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    P.timing(True)
+    P.timing_read()  # discard warm-up launches
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kernel_ms, launches = P.timing_read()
+    P.timing(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_bytes = batch_bytes * args.steps * world
+    value = total_bytes / elapsed / (1 << 30)
+    avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
+    achieved_gbs = batch_bytes / avg_kernel_s / 1e9
+
+    traffic = None
+    if args.profile_json and os.path.exists(args.profile_json):
+        prof = json.load(open(args.profile_json))
+        traffic = prof.get("hbm_bytes_per_launch")
+
+    line = {
+        "metric": "CRC32C GiB/s on device-resident object buffers (4 KiB–4 MiB), 1/2/4/8 GPUs",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (uniform random bytes, torch.randint on device), seed 0 per buffer",
+        "config": {"workload": desc, "buffers_per_gpu": n, "bytes_per_gpu_per_step": batch_bytes,
+                   "parallelism": f"shard{world} (independent buffers per GPU, no collective)",
+                   "kernel": P.version()},
+        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "pech_crc32c_main", "avg_launch_us": round(avg_kernel_s * 1e6, 2),
+                     "launches": launches},
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args, bufs[0], offs, sizes, outs, rotate, P)
+
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, buf0, offs, sizes, outs, rotate, P):
+    """Reference crc32c() on this host's cores over a bounded sample of the
+    same batch; also checks the GPU's outputs for the sampled buffers."""
+    import torch
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+
+    # recompute batch 0 on the GPU (outputs of the last timed step may be batch 1)
+    P.dev_batch_async(P.make_descs(buf0.data_ptr() + offs, sizes, device=buf0.device),
+                      outs[0])
+    torch.cuda.synchronize()
+    gpu = outs[0].cpu().numpy().view(np.uint32)
+    # sample: leading buffers of batch 0, about 256 MiB
+    k = int(np.searchsorted(np.cumsum(sizes), 256 << 20, side="right"))
+    k = max(1, min(k, len(sizes)))
+    nbytes = int(offs[k - 1] + sizes[k - 1])
+    host = buf0[:nbytes].cpu().numpy()
+    ref = O.ref()
+    kind = "reference" if ref is not None else "port"
+    fn = ref.ref_crc32c if ref is not None else O.oracle().oracle_crc32c
+    base = host.ctypes.data
+    res = np.zeros(k, dtype=np.uint32)
+    done_bytes = 0
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        for i in range(k):
+            res[i] = fn(0, base + int(offs[i]), int(sizes[i]))
+        done_bytes += nbytes
+        reps += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    if not np.array_equal(res, gpu[:k]):
+        bad = int(np.count_nonzero(res != gpu[:k]))
+        raise SystemExit(f"PARITY FAILURE: {bad}/{k} sampled buffers differ between GPU and reference")
+    cpu_model = ""
+    try:
+        for l in open("/proc/cpuinfo"):
+            if l.startswith("model name"):
+                cpu_model = l.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(done_bytes / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{k} leading buffers ({nbytes / (1 << 20):.0f} MiB) of batch 0, {reps} pass(es), "
+                      f"{dt:.1f} s, 1 thread, {cpu_model}; GPU outputs for the sample matched bit-exact"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+/*
+ * pech_crc32c.h -- batch / device / algebra API of libpech_crc32c.so.
+ *
+ * Every entry point computes exactly what the reference's per-buffer
+ * crc32c(seed, buf, len) (/root/reference/include/crc32c.h:88-96) returns;
+ * what changes is how many buffers one call covers and where the bytes live.
+ *
+ * Reference interfaces these replace or extend (file:line in /root/reference):
+ *   crc32c_batch          -- the per-payload loop of ceph_crc32c_iov()
+ *                            (src/ceph/messenger.c:1734-1740, driven from
+ *                            read_partial_msg_data :2677 and
+ *                            write_partial_message_data :1788): one call per
+ *                            completed payload instead of one per <=4 KiB
+ *                            piece (bit-identical by the chaining law).
+ *   crc32c_dev_batch_*    -- same, over device-resident buffers (GPU-resident
+ *                            object data; no reference counterpart).
+ *   crc32c_combine/_shift -- CRC reuse across replica sends
+ *                            (src/ceph/osd_server.c:1119 nested cursor,
+ *                            :1972 per-replica ceph_con_send) and page-piece
+ *                            joins (src/iov_iter.c:188-207).
+ *
+ * Conventions (pech style, include/err.h): int-returning calls give 0 or a
+ * negative errno: -EINVAL bad arguments, -ENOMEM allocation failure, -EIO a
+ * HIP failure (crc32c_last_error() has the text), -ENODEV no usable GPU.
+ * There is no CPU fallback: without a GPU every compute call fails loudly.
+ * Threading: one caller thread at a time per process (pech is one OS thread,
+ * README:11-16); HIP calls need more than pech's 64 KiB coroutine stacks
+ * (src/sched.c:16) -- see INTEGRATION.md.
+ */
+#ifndef PECH_CRC32C_H
+#define PECH_CRC32C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "crc32c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One device-resident buffer of a device batch (16 bytes, AoS). */
+struct crc32c_desc {
+	uint64_t addr; /* device address of the first byte (any alignment) */
+	uint32_t len;  /* bytes; 0 => result is seed                        */
+	uint32_t seed; /* incoming register, as crc32c()'s first argument    */
+};
+
+/* flags for crc32c_batch() */
+#define CRC32C_F_HOST 0u   /* bufs are pageable host memory                */
+#define CRC32C_F_DEVICE 1u /* bufs are device memory on the current device */
+#define CRC32C_F_PINNED 2u /* bufs are pinned host memory (DMA directly)   */
+
+/*
+ * out[i] = crc32c(seeds ? seeds[i] : 0, bufs[i], lens[i]) for i < n.
+ * Synchronous.  Host buffers are moved with hipMemcpyAsync through pinned
+ * staging (double-buffered, overlapped with the kernel); results come back
+ * with one D2H copy per sub-batch.
+ */
+int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
+		 uint32_t *out, unsigned int n, unsigned int flags);
+
+/*
+ * Device batch, asynchronous on `stream` (a hipStream_t, NULL = default
+ * stream): d_out[i] = crc32c(d_descs[i].seed, d_descs[i].addr, d_descs[i].len).
+ * d_descs and d_out are device memory of the current device; the call only
+ * enqueues work (no host synchronisation, no allocation once the internal
+ * workspace is large enough: see crc32c_dev_reserve()).  Buffers and
+ * descriptors must stay valid and unmodified until the stream reaches the
+ * end of the enqueued work.
+ */
+int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n,
+			   void *stream);
+
+/* Workspace the device batch needs for n buffers, and the explicit-workspace
+ * form (for concurrent streams or graph capture). */
+size_t crc32c_dev_workspace_bytes(unsigned int n);
+int crc32c_dev_batch_ws_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n,
+			      void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* Pre-size the internal workspace of the current device for n buffers. */
+int crc32c_dev_reserve(unsigned int n);
+
+/* Algebra (no data pass):
+ *   crc32c_shift(v, n)        == crc32c(v, <n zero bytes>, n)
+ *   crc32c_combine(a, b, lb)  == crc32c(s, A||B)  given a = crc32c(s, A),
+ *                                b = crc32c(0, B), lb = |B|.               */
+uint32_t crc32c_shift(uint32_t v, uint64_t nbytes);
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* Eagerly initialise the current device (tables, streams).  Optional. */
+int crc32c_device_init(void);
+
+/* Kernel timing: when enabled, HIP events bracket every main-kernel launch
+ * on its stream; crc32c_timing_read() synchronises on them and returns the
+ * summed kernel milliseconds and launch count since the last read. */
+int crc32c_timing(int enable);
+int crc32c_timing_read(double *kernel_ms, uint64_t *launches);
+
+/* Text of the last error (thread-local), "" if none. */
+const char *crc32c_last_error(void);
+
+/* Library / kernel identification, e.g. "pech_crc32c gfx950 rows128 ...". */
+const char *crc32c_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PECH_CRC32C_H */

@@ -1,0 +1,10 @@
+"""pech_amd -- MI355X-native (gfx950) CRC32C message-checksum path for pech.
+
+The product is libpech_crc32c.so (C-ABI: include/crc32c.h drop-in for
+/root/reference/include/crc32c.h:88, plus include/pech_crc32c.h batch/device
+API).  This package is its Python mirror for tests and benchmarks.
+"""
+from .crc32c import (  # noqa: F401
+    Crc32cError, crc32c, crc32c_batch, crc32c_combine, crc32c_shift, crc32c_tensors, dev_batch_async,
+    make_descs, shard_ranges, timing, timing_read, version,
+)

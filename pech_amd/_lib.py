@@ -1,0 +1,65 @@
+"""ctypes binding of libpech_crc32c.so (the C-ABI in include/*.h).
+
+The library is built in-tree by `make` (__graft_entry__.build()).  There is
+no fallback: if the shared library is missing or a symbol is absent, loading
+raises, and compute calls report the library's own error text.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpech_crc32c.so")
+
+_lib = None
+
+
+class Crc32cError(RuntimeError):
+    pass
+
+
+class CDesc(ctypes.Structure):
+    """struct crc32c_desc (include/pech_crc32c.h)."""
+    _fields_ = [("addr", ctypes.c_uint64), ("len", ctypes.c_uint32), ("seed", ctypes.c_uint32)]
+
+
+# name -> (restype, argtypes); must cover every function in include/*.h
+SIGNATURES = {
+    "crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint]),
+    "crc32c_batch": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint),
+                                     ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                     ctypes.c_uint, ctypes.c_uint]),
+    "crc32c_dev_batch_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
+    "crc32c_dev_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint]),
+    "crc32c_dev_batch_ws_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p,
+                                                 ctypes.c_size_t, ctypes.c_void_p]),
+    "crc32c_dev_reserve": (ctypes.c_int, [ctypes.c_uint]),
+    "crc32c_shift": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
+    "crc32c_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "crc32c_device_init": (ctypes.c_int, []),
+    "crc32c_timing": (ctypes.c_int, [ctypes.c_int]),
+    "crc32c_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+    "crc32c_last_error": (ctypes.c_char_p, []),
+    "crc32c_version": (ctypes.c_char_p, []),
+}
+
+
+def lib():
+    """Load (once) and return the C library; raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise Crc32cError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build()) first")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        err = lib().crc32c_last_error().decode(errors="replace")
+        raise Crc32cError(f"{what} failed ({rc}): {err}")
+    return rc

@@ -1,0 +1,147 @@
+"""Python mirror of the C-ABI (include/crc32c.h, include/pech_crc32c.h).
+
+Same names and argument meaning as the reference's crc32c()
+(/root/reference/include/crc32c.h:88): `crc` is the incoming raw register,
+the result is the raw register after the bytes, no inversion.  Device
+buffers are torch uint8 tensors on a ROCm device (torch is plumbing here:
+device memory and streams); every checksum is computed by the gfx950 kernel
+in libpech_crc32c.so.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import CDesc, Crc32cError, check, lib
+
+__all__ = [
+    "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
+    "crc32c_tensors", "shard_ranges", "Crc32cError", "timing", "timing_read", "version",
+]
+
+F_HOST, F_DEVICE, F_PINNED = 0, 1, 2
+
+
+def crc32c(crc, data):
+    """crc32c(crc, data) over host bytes (include/crc32c.h:88 semantics)."""
+    mv = memoryview(data).cast("B")
+    n = mv.nbytes
+    if n == 0:
+        return crc & 0xFFFFFFFF
+    buf = (ctypes.c_char * n).from_buffer_copy(mv) if mv.readonly else (ctypes.c_char * n).from_buffer(mv)
+    return lib().crc32c(crc & 0xFFFFFFFF, ctypes.addressof(buf), n)
+
+
+def crc32c_batch(bufs, seeds=None):
+    """One independent CRC per host buffer (bytes-like), as a list of ints."""
+    n = len(bufs)
+    if n == 0:
+        return []
+    keep = []
+    ptrs = (ctypes.c_void_p * n)()
+    lens = (ctypes.c_uint * n)()
+    for i, b in enumerate(bufs):
+        mv = memoryview(b).cast("B")
+        c = (ctypes.c_char * max(mv.nbytes, 1)).from_buffer_copy(mv.tobytes() or b"\0")
+        keep.append(c)
+        ptrs[i] = ctypes.addressof(c)
+        lens[i] = mv.nbytes
+    sd = None
+    if seeds is not None:
+        sd = (ctypes.c_uint32 * n)(*[s & 0xFFFFFFFF for s in seeds])
+    out = (ctypes.c_uint32 * n)()
+    check(lib().crc32c_batch(ptrs, lens, sd, out, n, F_HOST), "crc32c_batch")
+    return list(out)
+
+
+def crc32c_shift(v, nbytes):
+    return lib().crc32c_shift(v & 0xFFFFFFFF, nbytes)
+
+
+def crc32c_combine(crc_a, crc_b, len_b):
+    return lib().crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
+
+
+def make_descs(addrs, lens, seeds=None, device=None):
+    """Pack descriptors (struct crc32c_desc, 16 B each) into an int64 tensor
+    of shape (n, 2): [addr, len | seed << 32]; on `device` if given."""
+    import torch
+
+    addrs = np.asarray(addrs, dtype=np.uint64)
+    lens = np.asarray(lens, dtype=np.uint64)
+    seeds = np.zeros_like(lens) if seeds is None else np.asarray(seeds, dtype=np.uint64) & np.uint64(0xFFFFFFFF)
+    if np.any(lens > np.uint64(0xFFFFFFFF)):
+        raise ValueError("buffer length must fit unsigned int (crc32c.h:88)")
+    packed = np.empty((len(addrs), 2), dtype=np.uint64)
+    packed[:, 0] = addrs
+    packed[:, 1] = lens | (seeds << np.uint64(32))
+    t = torch.from_numpy(packed.view(np.int64).copy())
+    return t.to(device) if device is not None else t
+
+
+def dev_batch_async(descs, out, stream=None):
+    """Enqueue the device batch: descs (n,2) int64 device tensor from
+    make_descs, out (n,) int32/uint32 device tensor.  `stream` is a
+    torch.cuda.Stream (default: torch's current stream)."""
+    import torch
+
+    n = descs.shape[0]
+    if out.numel() < n or out.element_size() != 4:
+        raise ValueError("out must hold n 32-bit words")
+    if stream is None:
+        stream = torch.cuda.current_stream(descs.device)
+    check(lib().crc32c_dev_batch_async(descs.data_ptr(), out.data_ptr(), n, stream.cuda_stream),
+          "crc32c_dev_batch_async")
+
+
+def crc32c_tensors(tensors, seeds=None, offsets=None, lengths=None):
+    """CRCs of device uint8 tensors (optionally sub-ranges [off, off+len)).
+    Synchronous convenience wrapper; returns a list of ints."""
+    import torch
+
+    n = len(tensors)
+    if n == 0:
+        return []
+    dev = tensors[0].device
+    addrs = [t.data_ptr() + (offsets[i] if offsets else 0) for i, t in enumerate(tensors)]
+    lens = [lengths[i] if lengths else t.numel() * t.element_size() for i, t in enumerate(tensors)]
+    descs = make_descs(addrs, lens, seeds, device=dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        dev_batch_async(descs, out)
+        torch.cuda.current_stream(dev).synchronize()
+    return [int(x) & 0xFFFFFFFF for x in out.cpu().numpy().view(np.uint32)]
+
+
+def shard_ranges(lens, world):
+    """Contiguous, byte-balanced split of a batch over `world` GPUs
+    (greedy prefix split of sum(len)).  Returns [(lo, hi)]
+    index ranges covering [0, n) in order; empty ranges allowed."""
+    lens = np.asarray(lens, dtype=np.float64)
+    n = len(lens)
+    if world <= 0:
+        raise ValueError("world must be positive")
+    csum = np.concatenate([[0.0], np.cumsum(lens)])
+    total = csum[-1]
+    cuts = [0]
+    for r in range(1, world):
+        target = total * r / world
+        cut = int(np.searchsorted(csum, target, side="left"))
+        cuts.append(min(max(cut, cuts[-1]), n))
+    cuts.append(n)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def timing(enable=True):
+    check(lib().crc32c_timing(1 if enable else 0), "crc32c_timing")
+
+
+def timing_read():
+    """(kernel_ms, launches) of main-kernel launches since the last read."""
+    ms = ctypes.c_double()
+    cnt = ctypes.c_uint64()
+    check(lib().crc32c_timing_read(ctypes.byref(ms), ctypes.byref(cnt)), "crc32c_timing_read")
+    return ms.value, cnt.value
+
+
+def version():
+    return lib().crc32c_version().decode()

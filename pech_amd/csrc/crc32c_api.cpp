@@ -1,0 +1,561 @@
+// crc32c_api.cpp -- C-ABI of libpech_crc32c.so (include/crc32c.h,
+// include/pech_crc32c.h): per-device context, constant tables, launch
+// sequencing, host-memory staging pipeline.
+//
+// The only compute path is the gfx950 kernels in crc32c_kernels.hip; this
+// file moves bytes and descriptors and never checksums data on the CPU.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/pech_crc32c.h"
+#include "gf2.h"
+#include "layout.h"
+
+static_assert(sizeof(struct crc32c_desc) == sizeof(struct pech_desc), "descriptor ABI");
+static_assert(sizeof(struct crc32c_desc) == 16, "descriptor ABI");
+
+extern "C" hipError_t pech_launch_plan(const pech_desc *, uint32_t, uint32_t *, uint32_t *, uint32_t *,
+				       hipStream_t);
+extern "C" hipError_t pech_launch_main(const pech_desc *, uint32_t, const uint32_t *, const uint32_t *,
+				       const uint32_t *, uint32_t *, uint32_t, uint32_t, hipStream_t);
+
+// ---------------------------------------------------------------------------
+static thread_local char g_err[512];
+
+static void set_err(const char *fmt, ...)
+{
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(g_err, sizeof(g_err), fmt, ap);
+	va_end(ap);
+}
+
+#define HIP_TRY(expr)                                                                          \
+	do {                                                                                   \
+		hipError_t e_ = (expr);                                                        \
+		if (e_ != hipSuccess) {                                                        \
+			set_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+				__LINE__);                                                     \
+			return -EIO;                                                           \
+		}                                                                              \
+	} while (0)
+
+// ---------------------------------------------------------------------------
+// constant tables (host side, built once)
+static void build_consts(uint32_t *c)
+{
+	const uint64_t shifts[5] = {128, 4, 16, 32, 64}; // TAB128, TAB4, TAB16, TAB32, TAB64
+	for (int t = 0; t < 5; ++t) {
+		const uint32_t xk = gf2_x8n(shifts[t]);
+		for (uint32_t k = 0; k < 4; ++k)
+			for (uint32_t e = 0; e < 256; ++e)
+				c[t * 1024u + k * 256u + e] = gf2_mulmod(xk, e << (8 * k));
+	}
+	// POWR[i][j] = x^(8 * 128 * j * 64^i)
+	for (uint32_t i = 0; i < 5; ++i) {
+		const uint64_t unit = (uint64_t)PECH_ROW_BYTES << (6 * i);
+		const uint32_t base = gf2_x8n(unit);
+		uint32_t acc = CRC32C_ONE;
+		for (uint32_t j = 0; j < 64; ++j) {
+			c[PECH_C_POWR + 64 * i + j] = acc;
+			acc = gf2_mulmod(acc, base);
+		}
+	}
+	for (uint32_t z = 0; z < 32; ++z)
+		c[PECH_C_XINV + z] = gf2_xinv8n(z);
+}
+
+// ---------------------------------------------------------------------------
+struct TimedLaunch {
+	hipEvent_t a, b;
+};
+
+struct DevCtx {
+	int dev = -1;
+	int ncu = 0;
+	uint32_t *d_consts = nullptr;
+	// internal workspace for crc32c_dev_batch_async
+	void *d_ws = nullptr;
+	size_t ws_bytes = 0;
+	// synchronous host paths
+	hipStream_t s_comp = nullptr, s_copy = nullptr;
+	uint8_t *h_stage[2] = {nullptr, nullptr};
+	uint8_t *d_stage[2] = {nullptr, nullptr};
+	size_t stage_bytes = 0;
+	pech_desc *h_desc[2] = {nullptr, nullptr};
+	pech_desc *d_desc[2] = {nullptr, nullptr};
+	uint32_t *h_out[2] = {nullptr, nullptr};
+	uint32_t *d_out[2] = {nullptr, nullptr};
+	uint32_t desc_cap = 0;
+	hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+	// timing
+	std::vector<TimedLaunch> pending;
+	std::vector<TimedLaunch> free_events;
+};
+
+static std::mutex g_mu;
+static DevCtx g_ctx[64];
+static bool g_timing = false;
+static uint32_t g_host_consts[PECH_C_WORDS];
+static bool g_host_consts_ready = false;
+
+static const uint32_t *host_consts()
+{
+	if (!g_host_consts_ready) {
+		build_consts(g_host_consts);
+		g_host_consts_ready = true;
+	}
+	return g_host_consts;
+}
+
+static int ctx_get(DevCtx **out)
+{
+	int dev = 0;
+	hipError_t e = hipGetDevice(&dev);
+	if (e != hipSuccess) {
+		set_err("no usable GPU: hipGetDevice: %s", hipGetErrorString(e));
+		return -ENODEV;
+	}
+	if (dev < 0 || dev >= 64) {
+		set_err("device index %d out of range", dev);
+		return -ENODEV;
+	}
+	DevCtx *c = &g_ctx[dev];
+	if (c->dev < 0) {
+		hipDeviceProp_t prop;
+		HIP_TRY(hipGetDeviceProperties(&prop, dev));
+		c->ncu = prop.multiProcessorCount;
+		HIP_TRY(hipMalloc(&c->d_consts, PECH_C_WORDS * sizeof(uint32_t)));
+		HIP_TRY(hipMemcpy(c->d_consts, host_consts(), PECH_C_WORDS * sizeof(uint32_t), hipMemcpyHostToDevice));
+		HIP_TRY(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
+		HIP_TRY(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking));
+		for (int i = 0; i < 2; ++i) {
+			HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
+			HIP_TRY(hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
+		}
+		c->dev = dev;
+	}
+	*out = c;
+	return 0;
+}
+
+static size_t ws_bytes_for(unsigned int n)
+{
+	const size_t lrs = ((size_t)n * 4u + 255u) & ~(size_t)255u;
+	return lrs + PECH_MAX_CHUNKS * 4u;
+}
+
+static int ws_reserve(DevCtx *c, unsigned int n)
+{
+	const size_t need = ws_bytes_for(n < PECH_MAX_BATCH ? n : PECH_MAX_BATCH);
+	if (need <= c->ws_bytes)
+		return 0;
+	if (c->d_ws)
+		HIP_TRY(hipFree(c->d_ws));
+	c->d_ws = nullptr;
+	c->ws_bytes = 0;
+	HIP_TRY(hipMalloc(&c->d_ws, need));
+	c->ws_bytes = need;
+	return 0;
+}
+
+static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
+			size_t ws_bytes, hipStream_t stream)
+{
+	if (n == 0)
+		return 0;
+	for (unsigned int off = 0; off < n; off += PECH_MAX_BATCH) {
+		const unsigned int m = (n - off) < PECH_MAX_BATCH ? (n - off) : PECH_MAX_BATCH;
+		if (ws_bytes < ws_bytes_for(m)) {
+			set_err("workspace too small: %zu < %zu", ws_bytes, ws_bytes_for(m));
+			return -EINVAL;
+		}
+		uint32_t *lrs = (uint32_t *)ws;
+		uint32_t *partials = (uint32_t *)((char *)ws + (((size_t)m * 4u + 255u) & ~(size_t)255u));
+		HIP_TRY(pech_launch_plan(d_descs + off, m, lrs, partials, d_out + off, stream));
+		TimedLaunch tl{};
+		if (g_timing) {
+			if (!c->free_events.empty()) {
+				tl = c->free_events.back();
+				c->free_events.pop_back();
+			} else {
+				HIP_TRY(hipEventCreate(&tl.a));
+				HIP_TRY(hipEventCreate(&tl.b));
+			}
+			HIP_TRY(hipEventRecord(tl.a, stream));
+		}
+		HIP_TRY(pech_launch_main(d_descs + off, m, lrs, partials, c->d_consts, d_out + off, (uint32_t)c->ncu,
+					 PECH_RPG_MIN, stream));
+		if (g_timing) {
+			HIP_TRY(hipEventRecord(tl.b, stream));
+			c->pending.push_back(tl);
+		}
+	}
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// host staging: two slots of `bytes` pinned host + device memory each
+static int stage_reserve(DevCtx *c, size_t bytes, uint32_t ndesc)
+{
+	if (bytes > c->stage_bytes) {
+		for (int i = 0; i < 2; ++i) {
+			if (c->h_stage[i])
+				HIP_TRY(hipHostFree(c->h_stage[i]));
+			if (c->d_stage[i])
+				HIP_TRY(hipFree(c->d_stage[i]));
+			c->h_stage[i] = nullptr;
+			c->d_stage[i] = nullptr;
+		}
+		c->stage_bytes = 0;
+		for (int i = 0; i < 2; ++i) {
+			HIP_TRY(hipHostMalloc(&c->h_stage[i], bytes, hipHostMallocDefault));
+			HIP_TRY(hipMalloc(&c->d_stage[i], bytes));
+		}
+		c->stage_bytes = bytes;
+	}
+	if (ndesc > c->desc_cap) {
+		for (int i = 0; i < 2; ++i) {
+			if (c->h_desc[i])
+				HIP_TRY(hipHostFree(c->h_desc[i]));
+			if (c->d_desc[i])
+				HIP_TRY(hipFree(c->d_desc[i]));
+			if (c->h_out[i])
+				HIP_TRY(hipHostFree(c->h_out[i]));
+			if (c->d_out[i])
+				HIP_TRY(hipFree(c->d_out[i]));
+			c->h_desc[i] = nullptr;
+			c->d_desc[i] = nullptr;
+			c->h_out[i] = nullptr;
+			c->d_out[i] = nullptr;
+		}
+		c->desc_cap = 0;
+		for (int i = 0; i < 2; ++i) {
+			HIP_TRY(hipHostMalloc(&c->h_desc[i], (size_t)ndesc * sizeof(pech_desc), hipHostMallocDefault));
+			HIP_TRY(hipMalloc(&c->d_desc[i], (size_t)ndesc * sizeof(pech_desc)));
+			HIP_TRY(hipHostMalloc(&c->h_out[i], (size_t)ndesc * 4u, hipHostMallocDefault));
+			HIP_TRY(hipMalloc(&c->d_out[i], (size_t)ndesc * 4u));
+		}
+		c->desc_cap = ndesc;
+	}
+	return 0;
+}
+
+static const size_t STAGE_BYTES = 64u << 20;      // per slot
+static const uint32_t STAGE_DESCS = 1u << 16;     // per slot
+static const size_t PINNED_DIRECT_MIN = 64u << 10; // pinned buffers >= this are DMA'd in place
+
+// One sub-batch of host buffers into slot `s`: gather bytes, enqueue copy,
+// kernels and result copy.  Buffers must each fit the slot.
+static int enqueue_host_slot(DevCtx *c, int s, const void *const *bufs, const unsigned int *lens,
+			     const uint32_t *seeds, const uint32_t *chain_seed, unsigned int i0, unsigned int m,
+			     unsigned int flags)
+{
+	size_t off = 0;
+	size_t packed_lo = 0; // start of the pending host-packed run
+	for (unsigned int k = 0; k < m; ++k) {
+		const unsigned int i = i0 + k;
+		const size_t len = lens[i];
+		const bool direct = (flags & CRC32C_F_PINNED) && len >= PINNED_DIRECT_MIN;
+		if (direct) {
+			if (off > packed_lo)
+				HIP_TRY(hipMemcpyAsync(c->d_stage[s] + packed_lo, c->h_stage[s] + packed_lo,
+						       off - packed_lo, hipMemcpyHostToDevice, c->s_copy));
+			HIP_TRY(hipMemcpyAsync(c->d_stage[s] + off, bufs[i], len, hipMemcpyHostToDevice, c->s_copy));
+		} else if (len) {
+			memcpy(c->h_stage[s] + off, bufs[i], len);
+		}
+		c->h_desc[s][k].addr = (uint64_t)(uintptr_t)(c->d_stage[s] + off);
+		c->h_desc[s][k].len = (uint32_t)len;
+		c->h_desc[s][k].seed = chain_seed ? *chain_seed : (seeds ? seeds[i] : 0u);
+		off = (off + len + 255u) & ~(size_t)255u;
+		if (direct)
+			packed_lo = off;
+	}
+	if (off > packed_lo)
+		HIP_TRY(hipMemcpyAsync(c->d_stage[s] + packed_lo, c->h_stage[s] + packed_lo, off - packed_lo,
+				       hipMemcpyHostToDevice, c->s_copy));
+	HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(pech_desc), hipMemcpyHostToDevice,
+			       c->s_copy));
+	HIP_TRY(hipEventRecord(c->ev_copied[s], c->s_copy));
+	HIP_TRY(hipStreamWaitEvent(c->s_comp, c->ev_copied[s], 0));
+	int rc = ws_reserve(c, m);
+	if (rc)
+		return rc;
+	rc = launch_batch(c, c->d_desc[s], c->d_out[s], m, c->d_ws, c->ws_bytes, c->s_comp);
+	if (rc)
+		return rc;
+	HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
+	HIP_TRY(hipEventRecord(c->ev_done[s], c->s_comp));
+	return 0;
+}
+
+// A single host buffer larger than a slot: chunk it and chain the register
+// through the seed (crc32c(crc32c(s,A),B) == crc32c(s,A||B)).
+static int host_big(DevCtx *c, const void *buf, size_t len, uint32_t seed, uint32_t *out, unsigned int flags)
+{
+	const uint8_t *p = (const uint8_t *)buf;
+	uint32_t crc = seed;
+	while (len) {
+		const size_t m = len < c->stage_bytes ? len : c->stage_bytes;
+		const void *b = p;
+		const unsigned int l = (unsigned int)m;
+		int rc = enqueue_host_slot(c, 0, &b, &l, nullptr, &crc, 0, 1, flags);
+		if (rc)
+			return rc;
+		HIP_TRY(hipEventSynchronize(c->ev_done[0]));
+		crc = c->h_out[0][0];
+		p += m;
+		len -= m;
+	}
+	*out = crc;
+	return 0;
+}
+
+static int host_batch(DevCtx *c, const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
+		      uint32_t *out, unsigned int n, unsigned int flags)
+{
+	int rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
+	if (rc)
+		return rc;
+	// slot bookkeeping for the double buffer
+	unsigned int slot_i0[2] = {0, 0}, slot_m[2] = {0, 0};
+	bool busy[2] = {false, false};
+	int s = 0;
+	unsigned int i = 0;
+	auto drain = [&](int t) -> int {
+		if (!busy[t])
+			return 0;
+		HIP_TRY(hipEventSynchronize(c->ev_done[t]));
+		memcpy(out + slot_i0[t], c->h_out[t], (size_t)slot_m[t] * 4u);
+		busy[t] = false;
+		return 0;
+	};
+	while (i < n) {
+		if (lens[i] > c->stage_bytes) {
+			for (int t = 0; t < 2; ++t)
+				if ((rc = drain(t)))
+					return rc;
+			if ((rc = host_big(c, bufs[i], lens[i], seeds ? seeds[i] : 0u, &out[i], flags)))
+				return rc;
+			++i;
+			continue;
+		}
+		// fill slot s with as many buffers as fit
+		if ((rc = drain(s)))
+			return rc;
+		size_t bytes = 0;
+		unsigned int m = 0;
+		while (i + m < n && m < STAGE_DESCS && lens[i + m] <= c->stage_bytes) {
+			const size_t nb = (bytes + lens[i + m] + 255u) & ~(size_t)255u;
+			if (nb > c->stage_bytes)
+				break;
+			bytes = nb;
+			++m;
+		}
+		if ((rc = enqueue_host_slot(c, s, bufs, lens, seeds, nullptr, i, m, flags)))
+			return rc;
+		slot_i0[s] = i;
+		slot_m[s] = m;
+		busy[s] = true;
+		i += m;
+		s ^= 1;
+	}
+	for (int t = 0; t < 2; ++t)
+		if ((rc = drain(t)))
+			return rc;
+	return 0;
+}
+
+static int device_batch_sync(DevCtx *c, const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
+			     uint32_t *out, unsigned int n)
+{
+	int rc = stage_reserve(c, c->stage_bytes ? c->stage_bytes : STAGE_BYTES, STAGE_DESCS);
+	if (rc)
+		return rc;
+	for (unsigned int i0 = 0; i0 < n; i0 += STAGE_DESCS) {
+		const unsigned int m = (n - i0) < STAGE_DESCS ? (n - i0) : STAGE_DESCS;
+		for (unsigned int k = 0; k < m; ++k) {
+			c->h_desc[0][k].addr = (uint64_t)(uintptr_t)bufs[i0 + k];
+			c->h_desc[0][k].len = lens[i0 + k];
+			c->h_desc[0][k].seed = seeds ? seeds[i0 + k] : 0u;
+		}
+		HIP_TRY(hipMemcpyAsync(c->d_desc[0], c->h_desc[0], (size_t)m * sizeof(pech_desc), hipMemcpyHostToDevice,
+				       c->s_comp));
+		if ((rc = ws_reserve(c, m)))
+			return rc;
+		if ((rc = launch_batch(c, c->d_desc[0], c->d_out[0], m, c->d_ws, c->ws_bytes, c->s_comp)))
+			return rc;
+		HIP_TRY(hipMemcpyAsync(c->h_out[0], c->d_out[0], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
+		HIP_TRY(hipStreamSynchronize(c->s_comp));
+		memcpy(out + i0, c->h_out[0], (size_t)m * 4u);
+	}
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// exported C-ABI
+extern "C" {
+
+uint32_t crc32c(uint32_t crc, const void *data, unsigned int length)
+{
+	if (length == 0)
+		return crc; // include/crc32c.h:92: the loop body never runs
+	uint32_t out = 0;
+	int rc;
+	{
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		rc = ctx_get(&c);
+		if (!rc)
+			rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
+		if (!rc) {
+			const void *b = data;
+			const uint32_t s = crc;
+			rc = host_batch(c, &b, &length, &s, &out, 1, CRC32C_F_HOST);
+		}
+	}
+	if (rc) {
+		fprintf(stderr, "pech_crc32c: crc32c() failed (%d): %s\n", rc, g_err);
+		abort();
+	}
+	return out;
+}
+
+int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds, uint32_t *out,
+		 unsigned int n, unsigned int flags)
+{
+	if (n == 0)
+		return 0;
+	if (!bufs || !lens || !out || flags > (CRC32C_F_DEVICE | CRC32C_F_PINNED) ||
+	    ((flags & CRC32C_F_DEVICE) && (flags & CRC32C_F_PINNED))) {
+		set_err("crc32c_batch: invalid arguments");
+		return -EINVAL;
+	}
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (rc)
+		return rc;
+	if (flags & CRC32C_F_DEVICE)
+		return device_batch_sync(c, bufs, lens, seeds, out, n);
+	return host_batch(c, bufs, lens, seeds, out, n, flags);
+}
+
+size_t crc32c_dev_workspace_bytes(unsigned int n)
+{
+	return ws_bytes_for(n < PECH_MAX_BATCH ? n : PECH_MAX_BATCH);
+}
+
+int crc32c_dev_batch_ws_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n, void *d_ws,
+			      size_t ws_bytes, void *stream)
+{
+	if (n == 0)
+		return 0;
+	if (!d_descs || !d_out || !d_ws) {
+		set_err("crc32c_dev_batch_ws_async: invalid arguments");
+		return -EINVAL;
+	}
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (rc)
+		return rc;
+	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+int crc32c_dev_reserve(unsigned int n)
+{
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (rc)
+		return rc;
+	return ws_reserve(c, n);
+}
+
+int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n, void *stream)
+{
+	if (n == 0)
+		return 0;
+	if (!d_descs || !d_out) {
+		set_err("crc32c_dev_batch_async: invalid arguments");
+		return -EINVAL;
+	}
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (rc)
+		return rc;
+	if ((rc = ws_reserve(c, n)))
+		return rc;
+	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, c->d_ws, c->ws_bytes, (hipStream_t)stream);
+}
+
+uint32_t crc32c_shift(uint32_t v, uint64_t nbytes)
+{
+	return gf2_shift(v, nbytes);
+}
+
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b)
+{
+	return gf2_shift(crc_a, len_b) ^ crc_b;
+}
+
+int crc32c_device_init(void)
+{
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	return ctx_get(&c);
+}
+
+int crc32c_timing(int enable)
+{
+	std::lock_guard<std::mutex> lk(g_mu);
+	g_timing = enable != 0;
+	return 0;
+}
+
+int crc32c_timing_read(double *kernel_ms, uint64_t *launches)
+{
+	std::lock_guard<std::mutex> lk(g_mu);
+	double ms = 0;
+	uint64_t cnt = 0;
+	for (int d = 0; d < 64; ++d) {
+		DevCtx *c = &g_ctx[d];
+		for (auto &tl : c->pending) {
+			HIP_TRY(hipEventSynchronize(tl.b));
+			float t = 0;
+			HIP_TRY(hipEventElapsedTime(&t, tl.a, tl.b));
+			ms += t;
+			++cnt;
+			c->free_events.push_back(tl);
+		}
+		c->pending.clear();
+	}
+	if (kernel_ms)
+		*kernel_ms = ms;
+	if (launches)
+		*launches = cnt;
+	return 0;
+}
+
+const char *crc32c_last_error(void)
+{
+	return g_err;
+}
+
+const char *crc32c_version(void)
+{
+	return "pech_crc32c 0.1 gfx950 rows128 group8 lds-bank-replicated-A128";
+}
+
+} // extern "C"

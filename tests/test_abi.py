@@ -1,0 +1,96 @@
+"""The C-ABI library: loads, exports every function include/*.h declares, and
+its host-side algebra (shift/combine, no data pass) matches the oracle.
+No compute calls here -- those need a GPU (tests/test_gpu_parity.py)."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(REPO, "include")
+
+
+def declared_functions():
+    names = set()
+    for h in os.listdir(INCLUDE):
+        if not h.endswith(".h"):
+            continue
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(crc32c\w*)\s*\(", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_header_declares_dropin():
+    names = declared_functions()
+    assert "crc32c" in names
+    assert {"crc32c_batch", "crc32c_dev_batch_async", "crc32c_combine", "crc32c_shift"} <= names
+
+
+def test_library_exports_every_declared_symbol():
+    from pech_amd import _lib
+
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert set(_lib.SIGNATURES) >= declared_functions()
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH]).decode()
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert declared_functions() <= exported
+
+
+def test_dropin_header_compiles_as_pech_c():
+    # pech is gnu89 C (reference Makefile); the drop-in must compile there
+    src = '#include "crc32c.h"\n#include "pech_crc32c.h"\nint main(void){return (int)sizeof(struct crc32c_desc)-16;}\n'
+    exe = os.path.join(REPO, "build", "hdrcheck")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    r = subprocess.run(["gcc", "-std=gnu89", "-Wall", "-Werror", "-I" + INCLUDE, "-x", "c", "-", "-o", exe],
+                       input=src.encode(), capture_output=True)
+    assert r.returncode == 0, r.stderr.decode()
+    assert subprocess.run([exe]).returncode == 0
+
+
+def test_shift_combine_match_oracle():
+    from pech_amd import crc32c_combine, crc32c_shift
+
+    o = O.oracle()
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        v = int(rng.integers(0, 1 << 32))
+        n = int(rng.integers(0, 1 << 40))
+        assert crc32c_shift(v, n) == o.oracle_shift(v, n)
+        b = int(rng.integers(0, 1 << 32))
+        assert crc32c_combine(v, b, n) == o.oracle_combine(v, b, n)
+    a = rng.integers(0, 256, 5000, dtype=np.uint8)
+    assert crc32c_combine(O.crc(9, a[:1234]), O.crc(0, a[1234:]), 5000 - 1234) == O.crc(9, a)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="checks the no-GPU failure mode")
+def test_no_gpu_fails_loudly():
+    # without a GPU the batch API returns an error (no CPU fallback) ...
+    code = (
+        "import ctypes, sys\n"
+        "from pech_amd import _lib\n"
+        "L = _lib.lib()\n"
+        "out = (ctypes.c_uint32 * 1)()\n"
+        "p = (ctypes.c_void_p * 1)(ctypes.addressof(ctypes.create_string_buffer(b'abc')))\n"
+        "l = (ctypes.c_uint * 1)(3)\n"
+        "rc = L.crc32c_batch(p, l, None, out, 1, 0)\n"
+        "print(rc, L.crc32c_last_error().decode())\n"
+        "sys.exit(0 if rc < 0 else 1)\n"
+    )
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, timeout=120)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    # ... and the drop-in crc32c(), which cannot return an error, aborts
+    code2 = "from pech_amd import _lib\nimport ctypes\nb=ctypes.create_string_buffer(b'abc')\n" \
+            "print(_lib.lib().crc32c(0, ctypes.addressof(b), 3))\n"
+    r2 = subprocess.run([sys.executable, "-c", code2], cwd=REPO, capture_output=True, timeout=120)
+    assert r2.returncode != 0
+    assert b"crc32c() failed" in r2.stderr

@@ -1,0 +1,292 @@
+"""GPU parity: the gfx950 kernel (through the C-ABI) against the oracle and
+the golden vectors, bit-exact.  Run on an MI355X: pytest -m gpu."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from gen import splitmix_bytes, xorshift_bytes
+
+pytestmark = pytest.mark.gpu
+
+KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kat.json")))
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return torch, torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def P():
+    import pech_amd
+
+    return pech_amd
+
+
+def dev_crcs(torch, P, dbuf, offs, lens, seeds=None):
+    """kernel CRCs of dbuf[off:off+len] (dbuf: device uint8 tensor)."""
+    base = dbuf.data_ptr()
+    addrs = [base + int(o) for o in offs]
+    descs = P.make_descs(addrs, lens, seeds, device=dbuf.device)
+    out = torch.full((len(lens),), 0x5A5A5A5A, dtype=torch.int32, device=dbuf.device)
+    P.dev_batch_async(descs, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+def to_dev(torch, host_u8, dev):
+    return torch.from_numpy(np.ascontiguousarray(host_u8)).to(dev)
+
+
+def test_perm_lane_layout_known_answer(torch_dev, P):
+    torch, dev = torch_dev
+    d = b"123456789"
+    buf = to_dev(torch, np.frombuffer(d, dtype=np.uint8), dev)
+    got = dev_crcs(torch, P, buf, [0], [9], [0])
+    assert got[0] == 0x58E3FA20
+    got = dev_crcs(torch, P, buf, [0], [9], [0xFFFFFFFF])
+    assert (~int(got[0])) & 0xFFFFFFFF == 0xE3069283
+
+
+def test_appendix_a_device(torch_dev, P):
+    torch, dev = torch_dev
+    for row in KAT["appendix_a"]:
+        n = row["len"]
+        d = np.frombuffer(xorshift_bytes(n), dtype=np.uint8) if n else np.zeros(1, np.uint8)
+        buf = to_dev(torch, d, dev)
+        seeds = [int(s, 16) for s in row["crc"]]
+        got = dev_crcs(torch, P, buf, [0] * 3, [n] * 3, seeds)
+        assert [int(x) for x in got] == [row["crc"][f"{s:08x}"] for s in seeds], n
+
+
+def test_golden_vectors_unaligned_device(torch_dev, P):
+    torch, dev = torch_dev
+    stream = np.frombuffer(splitmix_bytes(0xC0FFEE, 3 * 65536 + 4096), dtype=np.uint8)
+    buf = to_dev(torch, stream, dev)
+    v = KAT["vectors"]
+    got = dev_crcs(torch, P, buf, [x["off"] for x in v], [x["len"] for x in v], [x["seed"] for x in v])
+    want = np.array([x["crc"] for x in v], dtype=np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(v[i], hex(got[i])) for i in bad[:10]]
+
+
+def test_each_vector_alone(torch_dev, P):
+    # single-buffer launches (one group, whole-buffer store path)
+    torch, dev = torch_dev
+    stream = np.frombuffer(splitmix_bytes(0xC0FFEE, 3 * 65536 + 4096), dtype=np.uint8)
+    buf = to_dev(torch, stream, dev)
+    for x in KAT["vectors"][::7]:
+        got = dev_crcs(torch, P, buf, [x["off"]], [x["len"]], [x["seed"]])
+        assert int(got[0]) == x["crc"], x
+
+
+def test_random_mixed_batch(torch_dev, P):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(1234)
+    n = 4000
+    lens = rng.integers(0, 20000, n)
+    lens[rng.random(n) < 0.1] = 0
+    tiny = rng.random(n) < 0.1
+    lens[tiny] = rng.integers(0, 40, int(tiny.sum()))
+    offs = np.zeros(n, dtype=np.int64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 64))
+        offs[i] = pos
+        pos += int(lens[i])
+    host = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+    seeds[rng.random(n) < 0.5] = 0
+    got = dev_crcs(torch, P, to_dev(torch, host, dev), offs, lens, seeds)
+    want = O.crcs(host, offs, lens, seeds)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(offs[i]), int(lens[i]), int(seeds[i]), hex(got[i]), hex(want[i])) for i in bad[:10]]
+
+
+def test_overlapping_and_repeated_buffers(torch_dev, P):
+    # descriptors may alias the same bytes; buffers are read only
+    torch, dev = torch_dev
+    rng = np.random.default_rng(99)
+    host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    offs = rng.integers(0, 1 << 19, 500)
+    lens = rng.integers(1, 1 << 19, 500)
+    got = dev_crcs(torch, P, to_dev(torch, host, dev), offs, lens)
+    assert np.array_equal(got, O.crcs(host, offs, lens))
+
+
+def test_c2_shape_full_parity(torch_dev, P):
+    # BASELINE config 2: 65,536 x 4 KiB device-resident buffers, every output checked
+    torch, dev = torch_dev
+    n, L = 65536, 4096
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    buf = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    offs = np.arange(n, dtype=np.int64) * L
+    got = dev_crcs(torch, P, buf, offs, [L] * n)
+    host = buf.cpu().numpy()
+    assert np.array_equal(got, O.crcs(host, offs, [L] * n))
+
+
+def test_c3_shape_parity(torch_dev, P):
+    # BASELINE config 3 shape: 4 MiB buffers (64 of them = 256 MiB), every output checked
+    torch, dev = torch_dev
+    n, L = 64, 4 << 20
+    buf = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+    offs = np.arange(n, dtype=np.int64) * L
+    got = dev_crcs(torch, P, buf, offs, [L] * n)
+    host = buf.cpu().numpy()
+    assert np.array_equal(got, O.crcs(host, offs, [L] * n))
+
+
+def test_c4_mixed_sizes_parity(torch_dev, P):
+    # config 4 mix (4 KiB / 64 KiB / 1 MiB / 4 MiB), shuffled, scaled to 128 MiB
+    torch, dev = torch_dev
+    rng = np.random.default_rng(42)
+    sizes = [4096] * 8192 + [65536] * 512 + [1 << 20] * 32 + [4 << 20] * 8
+    rng.shuffle(sizes)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    total = int(np.sum(sizes))
+    buf = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev)
+    got = dev_crcs(torch, P, buf, offs, sizes)
+    assert np.array_equal(got, O.crcs(buf.cpu().numpy(), offs, sizes))
+
+
+def test_single_huge_buffer_split_over_all_groups(torch_dev, P):
+    torch, dev = torch_dev
+    L = (96 << 20) + 12345
+    buf = torch.randint(0, 256, (L + 16,), dtype=torch.uint8, device=dev)
+    host = buf.cpu().numpy()
+    for off, seed in ((0, 0), (3, 0xFFFFFFFF), (11, 0x12345678)):
+        got = dev_crcs(torch, P, buf, [off], [L], [seed])
+        assert int(got[0]) == O.crc(seed, host[off:off + L])
+
+
+def test_sensitivity_constant_data(torch_dev, P):
+    torch, dev = torch_dev
+    for val in (0x00, 0xFF):
+        buf = torch.full((64 * 4096,), val, dtype=torch.uint8, device=dev)
+        got = dev_crcs(torch, P, buf, np.arange(64) * 4096, [4096] * 64)
+        want = KAT["checks"]["zeros4096_seed0" if val == 0 else "ff4096_seed0"]
+        assert all(int(x) == want for x in got)
+
+
+def test_chaining_and_linearity_at_full_size(torch_dev, P):
+    # size-independent properties on a 1 GiB buffer (no oracle needed):
+    #   crc(s, A||B) == combine(crc(s, A), crc(0, B), |B|)
+    #   crc(0, X ^ Y) == crc(0, X) ^ crc(0, Y)          (equal lengths)
+    torch, dev = torch_dev
+    L = 1 << 30
+    x = torch.randint(0, 256, (L,), dtype=torch.uint8, device=dev)
+    y = torch.randint(0, 256, (L,), dtype=torch.uint8, device=dev)
+    cut = 123456789
+    whole, a, b = dev_crcs(torch, P, x, [0, 0, cut], [L, cut, L - cut], [7, 7, 0])
+    assert P.crc32c_combine(int(a), int(b), L - cut) == int(whole)
+    xy = torch.bitwise_xor(x, y)
+    cx, cy, cxy = (int(dev_crcs(torch, P, t, [0], [L])[0]) for t in (x, y, xy))
+    assert cx ^ cy == cxy
+
+
+def test_empty_and_tiny(torch_dev, P):
+    torch, dev = torch_dev
+    host = np.arange(256, dtype=np.uint8)
+    buf = to_dev(torch, host, dev)
+    offs, lens, seeds = [], [], []
+    for off in range(0, 20):
+        for n in range(0, 6):
+            for s in (0, 0xA5A5A5A5):
+                offs.append(off)
+                lens.append(n)
+                seeds.append(s)
+    got = dev_crcs(torch, P, buf, offs, lens, seeds)
+    assert np.array_equal(got, O.crcs(host, offs, lens, seeds))
+    # all-empty batch: every output is its seed
+    got = dev_crcs(torch, P, buf, [0] * 10, [0] * 10, list(range(10)))
+    assert [int(x) for x in got] == list(range(10))
+
+
+def test_more_than_one_launch_of_buffers(torch_dev, P):
+    # > 2^20 descriptors: the library splits into several plan/main launches
+    torch, dev = torch_dev
+    n = (1 << 20) + 777
+    host = np.random.default_rng(5).integers(0, 256, n + 64, dtype=np.uint8)
+    offs = np.arange(n, dtype=np.int64)
+    lens = (np.arange(n) % 33).astype(np.int64)
+    got = dev_crcs(torch, P, to_dev(torch, host, dev), offs, lens)
+    assert np.array_equal(got, O.crcs(host, offs, lens))
+
+
+def test_dropin_crc32c_host_memory(P):
+    rng = np.random.default_rng(8)
+    for n in (1, 3, 4, 49, 4096, 100000):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for s in (0, 0xFFFFFFFF):
+            assert P.crc32c(s, d) == O.crc(s, d)
+    assert P.crc32c(0x1234, b"") == 0x1234
+
+
+def test_dropin_crc32c_larger_than_staging(P):
+    # > 64 MiB staging slot: chained through the seed inside the library
+    d = np.random.default_rng(9).integers(0, 256, (64 << 20) + 4097, dtype=np.uint8)
+    assert P.crc32c(0xFFFFFFFF, d) == O.crc(0xFFFFFFFF, d)
+
+
+def test_batch_host_pinned_device_flags(torch_dev, P):
+    torch, dev = torch_dev
+    from pech_amd import _lib
+
+    rng = np.random.default_rng(10)
+    lens = [int(x) for x in rng.integers(0, 300000, 64)] + [0, 1, 2, 70000]
+    bufs = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+    seeds = [int(x) for x in rng.integers(0, 1 << 32, len(lens))]
+    want = [O.crc(s, b) for s, b in zip(seeds, bufs)]
+    assert P.crc32c_batch([b.tobytes() for b in bufs], seeds) == want
+    L = _lib.lib()
+    n = len(lens)
+    # pinned host memory: DMA'd in place
+    pinned = [torch.from_numpy(b).pin_memory() if b.size else torch.zeros(1, dtype=torch.uint8).pin_memory()
+              for b in bufs]
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in pinned])
+    cl = (ctypes.c_uint * n)(*lens)
+    cs = (ctypes.c_uint32 * n)(*seeds)
+    out = (ctypes.c_uint32 * n)()
+    assert L.crc32c_batch(ptrs, cl, cs, out, n, 2) == 0
+    assert list(out) == want
+    # device memory through the synchronous batch call
+    dts = [t.to(dev) for t in pinned]
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dts])
+    out = (ctypes.c_uint32 * n)()
+    assert L.crc32c_batch(ptrs, cl, cs, out, n, 1) == 0
+    assert list(out) == want
+    # invalid flags
+    assert L.crc32c_batch(ptrs, cl, cs, out, n, 3) < 0
+
+
+def test_graph_capture_and_replay(torch_dev, P):
+    # the device batch enqueues no host sync / allocation: capturable
+    torch, dev = torch_dev
+    n, L = 256, 65536
+    buf = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+    offs = np.arange(n) * L
+    descs = P.make_descs([buf.data_ptr() + int(o) for o in offs], [L] * n, device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    from pech_amd import _lib
+
+    assert _lib.lib().crc32c_dev_reserve(n) == 0
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        P.dev_batch_async(descs, out, stream=s)  # warm-up outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        P.dev_batch_async(descs, out, stream=s)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), O.crcs(buf.cpu().numpy(), offs, [L] * n))
