@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpech_crc32c.so")
+# PECH_CRC32C_LIB selects an alternative build (A/B experiments only)
+LIB_PATH = os.environ.get("PECH_CRC32C_LIB") or os.path.join(HERE, "libpech_crc32c.so")
 
 _lib = None
 

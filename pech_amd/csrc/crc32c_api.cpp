@@ -22,10 +22,12 @@
 static_assert(sizeof(struct crc32c_desc) == sizeof(struct pech_desc), "descriptor ABI");
 static_assert(sizeof(struct crc32c_desc) == 16, "descriptor ABI");
 
-extern "C" hipError_t pech_launch_plan(const pech_desc *, uint32_t, uint32_t *, uint32_t *, uint32_t *,
-				       hipStream_t);
-extern "C" hipError_t pech_launch_main(const pech_desc *, uint32_t, const uint32_t *, const uint32_t *,
-				       const uint32_t *, uint32_t *, uint32_t, uint32_t, hipStream_t);
+extern "C" hipError_t pech_launch_plan(const pech_desc *, uint32_t, pech_core *, uint32_t *, uint32_t *, uint32_t *,
+				       const uint32_t *, uint32_t *, hipStream_t);
+extern "C" hipError_t pech_launch_main(const pech_core *, uint32_t, const uint32_t *, const uint32_t *,
+				       const uint32_t *, const uint32_t *, uint32_t *, uint32_t, uint32_t, hipStream_t);
+
+extern "C" const char *pech_kernel_tag(void);
 
 // ---------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -52,6 +54,7 @@ static void set_err(const char *fmt, ...)
 // constant tables (host side, built once)
 static void build_consts(uint32_t *c)
 {
+	// byte tables of A_n (advance n zero bytes): T_k[e] = A_n(e << 8k)
 	const uint64_t shifts[5] = {128, 4, 16, 32, 64}; // TAB128, TAB4, TAB16, TAB32, TAB64
 	for (int t = 0; t < 5; ++t) {
 		const uint32_t xk = gf2_x8n(shifts[t]);
@@ -59,18 +62,18 @@ static void build_consts(uint32_t *c)
 			for (uint32_t e = 0; e < 256; ++e)
 				c[t * 1024u + k * 256u + e] = gf2_mulmod(xk, e << (8 * k));
 	}
-	// POWR[i][j] = x^(8 * 128 * j * 64^i)
-	for (uint32_t i = 0; i < 5; ++i) {
-		const uint64_t unit = (uint64_t)PECH_ROW_BYTES << (6 * i);
-		const uint32_t base = gf2_x8n(unit);
+	// POWB[i][j] = x^(8 * j * 64^i)
+	for (uint32_t i = 0; i < 6; ++i) {
+		const uint32_t base = gf2_x8n((uint64_t)1 << (6 * i));
 		uint32_t acc = CRC32C_ONE;
 		for (uint32_t j = 0; j < 64; ++j) {
-			c[PECH_C_POWR + 64 * i + j] = acc;
+			c[PECH_C_POWB + 64 * i + j] = acc;
 			acc = gf2_mulmod(acc, base);
 		}
 	}
-	for (uint32_t z = 0; z < 32; ++z)
-		c[PECH_C_XINV + z] = gf2_xinv8n(z);
+	// A_1: the reference byte table (include/crc32c.h:16-81), regenerated
+	for (uint32_t e = 0; e < 256; ++e)
+		c[PECH_C_TAB1 + e] = gf2_mulmod(CRC32C_X8, e);
 }
 
 // ---------------------------------------------------------------------------
@@ -147,10 +150,11 @@ static int ctx_get(DevCtx **out)
 	return 0;
 }
 
+// workspace: cores[nch*1024] | lrs[nch*1024] | partials[1024] | nzs[1024]
 static size_t ws_bytes_for(unsigned int n)
 {
-	const size_t lrs = ((size_t)n * 4u + 255u) & ~(size_t)255u;
-	return lrs + PECH_MAX_CHUNKS * 4u;
+	const size_t slots = (size_t)((n + PECH_CHUNK - 1) / PECH_CHUNK) * PECH_CHUNK;
+	return slots * (sizeof(pech_core) + 4u) + 2u * PECH_MAX_CHUNKS * 4u;
 }
 
 static int ws_reserve(DevCtx *c, unsigned int n)
@@ -178,9 +182,12 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			set_err("workspace too small: %zu < %zu", ws_bytes, ws_bytes_for(m));
 			return -EINVAL;
 		}
-		uint32_t *lrs = (uint32_t *)ws;
-		uint32_t *partials = (uint32_t *)((char *)ws + (((size_t)m * 4u + 255u) & ~(size_t)255u));
-		HIP_TRY(pech_launch_plan(d_descs + off, m, lrs, partials, d_out + off, stream));
+		const size_t slots = (size_t)((m + PECH_CHUNK - 1) / PECH_CHUNK) * PECH_CHUNK;
+		pech_core *cores = (pech_core *)ws;
+		uint32_t *lrs = (uint32_t *)(cores + slots);
+		uint32_t *partials = lrs + slots;
+		uint32_t *nzs = partials + PECH_MAX_CHUNKS;
+		HIP_TRY(pech_launch_plan(d_descs + off, m, cores, lrs, partials, nzs, c->d_consts, d_out + off, stream));
 		TimedLaunch tl{};
 		if (g_timing) {
 			if (!c->free_events.empty()) {
@@ -192,8 +199,8 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			}
 			HIP_TRY(hipEventRecord(tl.a, stream));
 		}
-		HIP_TRY(pech_launch_main(d_descs + off, m, lrs, partials, c->d_consts, d_out + off, (uint32_t)c->ncu,
-					 PECH_RPG_MIN, stream));
+		HIP_TRY(pech_launch_main(cores, m, lrs, partials, nzs, c->d_consts, d_out + off, (uint32_t)c->ncu,
+					 PECH_RPW_MIN, stream));
 		if (g_timing) {
 			HIP_TRY(hipEventRecord(tl.b, stream));
 			c->pending.push_back(tl);
@@ -555,7 +562,7 @@ const char *crc32c_last_error(void)
 
 const char *crc32c_version(void)
 {
-	return "pech_crc32c 0.1 gfx950 rows128 group8 lds-bank-replicated-A128";
+	return pech_kernel_tag();
 }
 
 } // extern "C"

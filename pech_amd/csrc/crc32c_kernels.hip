@@ -1,65 +1,71 @@
 // crc32c_kernels.hip -- gfx950 (CDNA4) kernels for batched CRC32C.
 //
-// Computes, for every descriptor (addr, len, seed) of a batch, exactly the
-// value of the reference crc32c(seed, addr, len)
-// (/root/reference/include/crc32c.h:88-96), over device-resident bytes.
+// For every descriptor (addr, len, seed) of a batch, computes exactly the
+// reference's crc32c(seed, addr, len) (/root/reference/include/crc32c.h:88-96)
+// over device-resident bytes.  Two launches per batch on the caller's stream:
 //
-// Two launches per batch, both on the caller's stream:
-//   pech_crc32c_plan : one 1024-thread workgroup per chunk of 1024 buffers;
-//                      rows per buffer (layout.h), chunk-local exclusive scan
-//                      -> lrs[], chunk totals -> partials[], out[] initialised
-//                      (0, or the seed for len == 0: crc32c.h:92 loop never runs).
-//   pech_crc32c_main : persistent, one 1024-thread workgroup per CU (the LDS
-//                      tables take 144 KiB).  Each 8-lane group walks a
-//                      contiguous range of rows of the batch's row space.
+//  pech_crc32c_plan  one 1024-thread workgroup per chunk of 1024 buffers:
+//      splits each buffer into head / core / tail (layout.h), checksums the
+//      <16-byte head and tail and the seed term itself (byte loop on the
+//      reference table + GF(2) shifts) and writes that partial result to out[],
+//      orders the chunk's buffers by size class (LDS counting sort) and writes
+//      core descriptors + the chunk-local exclusive scan of core rows.
 //
-// Hot loop (per lane, per 128-byte row): one coalesced 16-byte load of its
-// piece, then for each of its 4 word streams  s <- A_128(s) ^ w, where
-// A_128 (advance 128 zero bytes) is four byte-indexed table lookups.  The
-// tables are replicated 32x in LDS, one copy per bank, so a lookup is
-// conflict-free whatever the data: lane l (mod 32) only ever touches bank l.
-// The byte -> LDS address step is ONE v_perm_b32 (byte k of s lands in
-// address byte 1, the lane's bank offset in byte 0).
-// A segment ends at a buffer end or at the group's range end; its 32 stream
-// registers are folded with single-copy A_4/A_16/A_32/A_64 tables, shifted
-// to the buffer's end with the power tables, and stored (whole buffer) or
-// xor-ed atomically (buffer split over groups) into out[].
+//  pech_crc32c_main  persistent, one 1024-thread workgroup per CU (the LDS
+//      tables take 144 KiB).  Each wave owns a contiguous range of the batch's
+//      row space and walks it in "steps"; a step gives each of the wave's 8
+//      lane-groups a run of rows of one buffer -- eight neighbouring buffers
+//      (small ones), or eight slices of one large buffer.  Per row and lane:
+//      one 16-byte load of its piece (rows = 128-byte lines, fully coalesced
+//      per group), then for its 4 word streams  s <- A_128(s) ^ w, where
+//      A_128 ("advance 128 zero bytes") is 4 byte-indexed table lookups.  The
+//      A_128 tables sit in LDS once per bank (32 copies), so lane l (mod 32)
+//      only ever reads bank l: conflict-free whatever the data; the byte ->
+//      LDS address step is ONE v_perm_b32.  Loads run PECH_U rows ahead with
+//      unconditional (clamped) addresses so waits are counted, not drained.
+//      At a run's end the 32 stream registers of a group are folded (A_4, then
+//      an A_16/A_32/A_64 butterfly over the 8 lanes), shifted to the buffer's
+//      end (x^(8m), power tables) and xor-ed atomically into out[].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "gf2.h"
 #include "layout.h"
 
-// ---- LDS map (bytes) ------------------------------------------------------
-#define L_REP 0u                      // 128 KiB: A_128 tables, 32 bank copies
-#define L_TAB4 131072u                // 4 KiB each, single copy
+#ifndef PECH_U
+#define PECH_U 8 // rows in flight per lane
+#endif
+
+// ---- LDS map of the main kernel (bytes) ---------------------------------
+#define L_REP 0u                 // 128 KiB: A_128, 32 bank copies
+#define L_TAB4 131072u           // 4 KiB each, single copy
 #define L_TAB16 (L_TAB4 + 4096u)
 #define L_TAB32 (L_TAB16 + 4096u)
 #define L_TAB64 (L_TAB32 + 4096u)
-#define L_POWR (L_TAB64 + 4096u)      // 1280 B
-#define L_XINV (L_POWR + 1280u)       // 128 B
-#define L_CHUNK (L_XINV + 128u)       // 4 KiB: chunk row offsets
-#define L_MISC (L_CHUNK + 4096u)      // scan scratch
+#define L_POWB (L_TAB64 + 4096u) // 1536 B
+#define L_CHUNK (L_POWB + 1536u) // 4 KiB: chunk row offsets
+#define L_NZ (L_CHUNK + 4096u)   // 4 KiB: chunk non-empty counts
+#define L_MISC (L_NZ + 4096u)    // scan scratch
 #define L_BYTES (L_MISC + 128u)
 
-static_assert(L_CHUNK == 131072u + 4u * (PECH_C_WORDS - PECH_C_TAB4), "LDS/consts layout mismatch");
+static_assert(L_POWB - L_TAB4 == 4u * (PECH_C_POWB - PECH_C_TAB4), "LDS/consts layout mismatch");
 static_assert(L_BYTES <= 160u * 1024u, "LDS budget");
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
-
-// 16-byte descriptor load through the global (not flat) address space
-__device__ __forceinline__ pech_desc load_desc(const pech_desc *descs, uint32_t b)
-{
-	const u32x4 v = *(g_u32x4 *)(descs + b);
-	pech_desc d;
-	d.addr = (uint64_t)v.x | ((uint64_t)v.y << 32);
-	d.len = v.z;
-	d.seed = v.w;
-	return d;
-}
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
 
 // ---- helpers --------------------------------------------------------------
+__device__ __forceinline__ uint32_t uni(uint32_t v)
+{
+	return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+	return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
 // 1024-thread exclusive scan; scratch = 16 LDS words
 __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t *total)
 {
@@ -67,7 +73,7 @@ __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32
 	uint32_t x = v;
 #pragma unroll
 	for (uint32_t d = 1; d < 64; d <<= 1) {
-		uint32_t y = __shfl_up(x, d);
+		const uint32_t y = __shfl_up(x, d);
 		if (lane >= d)
 			x += y;
 	}
@@ -76,8 +82,8 @@ __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32
 	__syncthreads();
 	uint32_t off = 0, tot = 0;
 #pragma unroll
-	for (uint32_t w = 0; w < PECH_WG_THREADS / 64u; ++w) {
-		uint32_t t = scratch[w];
+	for (uint32_t w = 0; w < PECH_WAVES_PER_WG; ++w) {
+		const uint32_t t = scratch[w];
 		off += (w < wave) ? t : 0u;
 		tot += t;
 	}
@@ -92,7 +98,7 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_o
 }
 
 // A_128(s) from the bank-replicated tables.  lreg = (lane&31)*4 | 1<<16.
-// table k, entry e, bank copy c lives at (k>>1)*64K + e*256 + (k&1)*128 + 4c.
+// Table k, entry e, bank copy c lives at (k>>1)*64K + e*256 + (k&1)*128 + 4c.
 __device__ __forceinline__ uint32_t adv128(const uint32_t *lds, uint32_t s, uint32_t lreg)
 {
 	const uint32_t a0 = __builtin_amdgcn_perm(s, lreg, 0x0C0C0400u);
@@ -109,331 +115,416 @@ __device__ __forceinline__ uint32_t adv_tab(const uint32_t *lds, uint32_t tab, u
 	return t[v & 0xFFu] ^ t[256u + ((v >> 8) & 0xFFu)] ^ t[512u + ((v >> 16) & 0xFFu)] ^ t[768u + (v >> 24)];
 }
 
-__device__ __forceinline__ uint32_t bytes_mask(int t) // low t bytes set, t in [0,4]
+// v * x^(8m) mod P with the 64-ary power table POWB[i][j] = x^(8 j 64^i)
+__device__ inline uint32_t shift_bytes(const uint32_t *powb, uint64_t m, uint32_t v)
 {
-	return t >= 4 ? 0xFFFFFFFFu : ((1u << (8 * t)) - 1u);
-}
-
-// Mask bytes of the piece at pa that lie outside [ptr, ptr+len) and xor the
-// seed into bytes [ptr, ptr+4).  Only rows at a buffer's edges get here.
-__device__ inline u32x4 fix_piece(u32x4 w, uint64_t pa, uint64_t ptr, uint32_t len, uint32_t seed)
-{
-	const int64_t dlo = (int64_t)(ptr - pa);
-	const int64_t dhi = (int64_t)(ptr + len - pa);
-	const int lo = (int)(dlo < 0 ? 0 : (dlo > 16 ? 16 : dlo));
-	const int hi = (int)(dhi < 0 ? 0 : (dhi > 16 ? 16 : dhi));
-	uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-	for (int k = 0; k < 4; ++k) {
-		const int a = max(lo - 4 * k, 0), b = min(hi - 4 * k, 4);
-		const uint32_t m = (b <= a) ? 0u : (bytes_mask(b) & ~bytes_mask(a));
-		ws[k] &= m;
-		const int64_t ds = dlo - 4 * k;
-		if (ds >= 0 && ds <= 3)
-			ws[k] ^= seed << (8 * (int)ds);
-		else if (ds >= -3 && ds < 0)
-			ws[k] ^= seed >> (-8 * (int)ds);
+	for (uint32_t i = 0; i < 6; ++i) {
+		const uint32_t d = (uint32_t)(m >> (6u * i)) & 63u;
+		if (d)
+			v = gf2_mulmod(powb[64u * i + d], v);
 	}
-	return (u32x4){ws[0], ws[1], ws[2], ws[3]};
+	return v;
 }
 
 // ---- plan kernel ----------------------------------------------------------
-extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
-	const pech_desc *__restrict__ descs, uint32_t n, uint32_t *__restrict__ lrs,
-	uint32_t *__restrict__ partials, uint32_t *__restrict__ out)
+// byte-wise reference update (include/crc32c.h:92-93) on the LDS table
+__device__ inline uint32_t crc_bytes(const uint32_t *t1, uint32_t crc, uint64_t addr, uint32_t n)
 {
-	__shared__ uint32_t scratch[PECH_WG_THREADS / 64u];
-	const uint32_t b = blockIdx.x * PECH_CHUNK + threadIdx.x;
-	uint32_t rows = 0;
+	const g_u8 *q = (const g_u8 *)addr;
+	for (uint32_t i = 0; i < n; ++i)
+		crc = t1[(crc ^ q[i]) & 0xFFu] ^ (crc >> 8);
+	return crc;
+}
+
+extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
+	const pech_desc *__restrict__ descs, uint32_t n, pech_core *__restrict__ cores, uint32_t *__restrict__ lrs,
+	uint32_t *__restrict__ partials, uint32_t *__restrict__ nzs, const uint32_t *__restrict__ consts,
+	uint32_t *__restrict__ out)
+{
+	__shared__ uint32_t t1[256];
+	__shared__ uint32_t powb[384];
+	__shared__ uint32_t hist[PECH_NCLASS], cursor[PECH_NCLASS];
+	__shared__ uint32_t rows_at[PECH_CHUNK];
+	__shared__ uint32_t scratch[PECH_WAVES_PER_WG];
+	const uint32_t tid = threadIdx.x;
+	if (tid < 256)
+		t1[tid] = consts[PECH_C_TAB1 + tid];
+	if (tid < 384)
+		powb[tid] = consts[PECH_C_POWB + tid];
+	if (tid < PECH_NCLASS)
+		hist[tid] = 0;
+	rows_at[tid] = 0;
+	__syncthreads();
+
+	const uint32_t b = blockIdx.x * PECH_CHUNK + tid;
+	uint32_t rows = 0, cls = 0;
+	pech_core core = {0, 0, 0};
 	if (b < n) {
 		const pech_desc d = descs[b];
-		rows = pech_rows(d.addr, d.len);
-		out[b] = d.len ? 0u : d.seed;
+		const uint64_t end = d.addr + d.len;
+		rows = pech_core_rows(d.addr, d.len);
+		uint32_t res;
+		if (rows == 0) {
+			// no full aligned piece: the whole buffer here (<= 30 bytes)
+			res = crc_bytes(t1, d.seed, d.addr, d.len);
+		} else {
+			const uint64_t cs = (d.addr + 15) & ~(uint64_t)15;
+			const uint64_t ce = end & ~(uint64_t)15;
+			const uint32_t h = (uint32_t)(cs - d.addr), t = (uint32_t)(end - ce);
+			res = 0;
+			if (d.seed)
+				res ^= shift_bytes(powb, d.len, d.seed);
+			if (h)
+				res ^= shift_bytes(powb, (uint64_t)d.len - h, crc_bytes(t1, 0, d.addr, h));
+			if (t)
+				res ^= crc_bytes(t1, 0, ce, t);
+			const uint32_t vp = rows * 8u - (uint32_t)((ce - cs) >> 4);
+			core.vbase = ce - (uint64_t)PECH_ROW_BYTES * rows;
+			core.rows = rows;
+			core.meta = PECH_META(b, vp, t);
+			cls = pech_size_class(rows);
+			atomicAdd(&hist[cls], 1u);
+		}
+		out[b] = res;
 	}
+	__syncthreads();
+	if (tid == 0) {
+		uint32_t acc = 0;
+		for (uint32_t c = 0; c < PECH_NCLASS; ++c) {
+			cursor[c] = acc;
+			acc += hist[c];
+		}
+		nzs[blockIdx.x] = acc;
+	}
+	__syncthreads();
+	if (rows) {
+		const uint32_t pos = atomicAdd(&cursor[cls], 1u);
+		cores[blockIdx.x * PECH_CHUNK + pos] = core;
+		rows_at[pos] = rows;
+	}
+	__syncthreads();
 	uint32_t total;
-	const uint32_t ex = block_excl_scan(rows, scratch, &total);
-	if (b < n)
-		lrs[b] = ex;
-	if (threadIdx.x == 0)
+	const uint32_t ex = block_excl_scan(rows_at[tid], scratch, &total);
+	lrs[blockIdx.x * PECH_CHUNK + tid] = ex;
+	if (tid == 0)
 		partials[blockIdx.x] = total;
 }
 
 // ---- main kernel ----------------------------------------------------------
-#ifndef PECH_PREFETCH
-#define PECH_PREFETCH 4 // rows in flight per lane
+// One run of rows per lane-group: `ad` = address of this lane's piece in the
+// run's first row, `nl` rows to load (>= 1), `nu` rows to use (0 = idle
+// group: loads repeat another group's rows, state ignored), `zoff` != 0 =
+// the first row's piece is a virtual zero (it may lie before the buffer, so
+// row 0 is loaded from ad + zoff -- the first real piece -- and zeroed).
+// T / nmin: max / min of nu over the wave's active groups (uniform).
+// The address is laundered through an empty asm: row 0 of a virtual piece is
+// zeroed after its load, and without the barrier LLVM treats the load's
+// address as "don't care" in that case and folds ad + zoff back to ad -- a
+// read before the buffer (seen in the ISA; a GPU fault at allocation starts).
+__device__ __forceinline__ uint64_t row_addr(uint64_t ad, uint32_t row, uint32_t zoff)
+{
+	uint64_t a = ad + (uint64_t)row * PECH_ROW_BYTES + (row == 0 ? zoff : 0u);
+	asm("" : "+v"(a));
+	return a;
+}
+
+#ifdef PECH_DEBUG_BOUNDS
+// debug build: every ring load is checked against the core [lo, hi) of the
+// buffer being walked; a violation is printed and redirected to lo.
+__device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, uint32_t tag)
+{
+	if (a < lo || a + 16u > hi) {
+		printf("PECH OOB tag %u blk %u tid %u addr %llx lo %llx hi %llx\n", tag, blockIdx.x, threadIdx.x,
+		       (unsigned long long)a, (unsigned long long)lo, (unsigned long long)hi);
+		a = lo;
+	}
+	return *(g_u32x4 *)a;
+}
+#define LD_PIECE(a, tag) ld_piece((a), blo, bhi, (tag))
+#else
+#define LD_PIECE(a, tag) (*(g_u32x4 *)(a))
 #endif
 
-struct LoadCur {
-	uint64_t pa;   // this lane's piece in the current row
-	uint64_t a0;   // pieces below a0 are virtual zeros
-	uint32_t left; // rows left in the buffer, current included
-	uint32_t b;
-	pech_desc nd;  // prefetched descriptor of buffer b+1
-};
+__device__ __forceinline__ void run_rows(const uint32_t *lds, uint32_t lreg, uint64_t ad, uint32_t nl, uint32_t nu,
+					 uint32_t zoff, uint32_t T, uint32_t nmin, uint32_t &s0, uint32_t &s1,
+					 uint32_t &s2, uint32_t &s3, uint64_t blo, uint64_t bhi)
+{
+	constexpr uint32_t U = PECH_U;
+	const uint32_t last = nl - 1u;
+	u32x4 ring[U];
+#pragma unroll
+	for (uint32_t i = 0; i < U; ++i)
+		ring[i] = LD_PIECE(row_addr(ad, min(i, last), zoff), 1);
+	if (zoff)
+		ring[0] = (u32x4)(0u);
+	s0 = s1 = s2 = s3 = 0;
+	const uint32_t nblk = (T + U - 1) / U;
+	uint32_t blk = 0;
+	// full blocks: every lane's rows valid, prefetch stays inside every run
+	for (; blk + 1 < nblk && (blk + 2) * U <= nmin; ++blk) {
+		const uint64_t base = ad + (uint64_t)(blk + 1) * U * PECH_ROW_BYTES;
+#pragma unroll
+		for (uint32_t i = 0; i < U; ++i) {
+			const u32x4 w = ring[i];
+			ring[i] = LD_PIECE(base + i * PECH_ROW_BYTES, 2);
+			s0 = adv128(lds, s0, lreg) ^ w.x;
+			s1 = adv128(lds, s1, lreg) ^ w.y;
+			s2 = adv128(lds, s2, lreg) ^ w.z;
+			s3 = adv128(lds, s3, lreg) ^ w.w;
+		}
+	}
+	// ragged blocks: clamped prefetch, predicated update
+	for (; blk + 1 < nblk; ++blk) {
+		const uint32_t r = blk * U;
+#pragma unroll
+		for (uint32_t i = 0; i < U; ++i) {
+			const u32x4 w = ring[i];
+			ring[i] = LD_PIECE(row_addr(ad, min(r + U + i, last), zoff), 3);
+			const bool ok = r + i < nu;
+			const uint32_t t0 = adv128(lds, s0, lreg) ^ w.x;
+			const uint32_t t1 = adv128(lds, s1, lreg) ^ w.y;
+			const uint32_t t2 = adv128(lds, s2, lreg) ^ w.z;
+			const uint32_t t3 = adv128(lds, s3, lreg) ^ w.w;
+			s0 = ok ? t0 : s0;
+			s1 = ok ? t1 : s1;
+			s2 = ok ? t2 : s2;
+			s3 = ok ? t3 : s3;
+		}
+	}
+	// last block: no more loads
+	{
+		const uint32_t r = blk * U;
+#pragma unroll
+		for (uint32_t i = 0; i < U; ++i) {
+			const u32x4 w = ring[i];
+			const bool ok = r + i < nu;
+			const uint32_t t0 = adv128(lds, s0, lreg) ^ w.x;
+			const uint32_t t1 = adv128(lds, s1, lreg) ^ w.y;
+			const uint32_t t2 = adv128(lds, s2, lreg) ^ w.z;
+			const uint32_t t3 = adv128(lds, s3, lreg) ^ w.w;
+			s0 = ok ? t0 : s0;
+			s1 = ok ? t1 : s1;
+			s2 = ok ? t2 : s2;
+			s3 = ok ? t3 : s3;
+		}
+	}
+}
 
-struct CompCur {
-	uint64_t pa;
-	uint64_t ptr;
-	uint32_t len, seed;
-	uint32_t lr, rows, z;
-	uint32_t b, seg0;
-	uint32_t edge;
-	pech_desc nd;
-};
+// Fold a group's 32 stream registers into the CRC of its run (as a message
+// ending at the run's last row), shift it to the buffer's core end plus the
+// tail (m bytes), xor into out[orig].
+__device__ __forceinline__ void finish_run(const uint32_t *lds, uint32_t g8, uint32_t s0, uint32_t s1, uint32_t s2,
+					   uint32_t s3, uint64_t m, bool active, uint32_t *out, uint32_t orig)
+{
+	uint32_t u = adv_tab(lds, L_TAB4, s0) ^ s1;
+	u = adv_tab(lds, L_TAB4, u) ^ s2;
+	u = adv_tab(lds, L_TAB4, u) ^ s3;
+	u = adv_tab(lds, L_TAB4, u);
+	uint32_t o, lo, hi;
+	o = __shfl_xor(u, 1);
+	lo = (g8 & 1u) ? o : u;
+	hi = (g8 & 1u) ? u : o;
+	u = adv_tab(lds, L_TAB16, lo) ^ hi;
+	o = __shfl_xor(u, 2);
+	lo = (g8 & 2u) ? o : u;
+	hi = (g8 & 2u) ? u : o;
+	u = adv_tab(lds, L_TAB32, lo) ^ hi;
+	o = __shfl_xor(u, 4);
+	lo = (g8 & 4u) ? o : u;
+	hi = (g8 & 4u) ? u : o;
+	u = adv_tab(lds, L_TAB64, lo) ^ hi;
+	if (active && g8 == 0) {
+		if (m)
+			u = shift_bytes(lds + L_POWB / 4u, m, u);
+		atomicXor(out + orig, u);
+	}
+}
 
 extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_main(
-	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ lrs,
-	const uint32_t *__restrict__ partials, uint32_t nchunks, const uint32_t *__restrict__ consts,
-	uint32_t *__restrict__ out, uint32_t rpg_min)
+	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
+	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts,
+	uint32_t *__restrict__ out, uint32_t rpw_min)
 {
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	const uint32_t tid = threadIdx.x;
 
-	// chunk row offsets and the batch's total row count
+	// chunk row offsets, non-empty counts and the batch's total row count
 	uint32_t Rtot;
 	{
 		const uint32_t pv = tid < nchunks ? partials[tid] : 0u;
+		lds[L_NZ / 4u + tid] = tid < nchunks ? nzs[tid] : 0u;
 		const uint32_t ex = block_excl_scan(pv, lds + L_MISC / 4u, &Rtot);
 		lds[L_CHUNK / 4u + tid] = ex;
 	}
-	const uint64_t G = (uint64_t)gridDim.x * PECH_GROUPS_PER_WG;
-	uint64_t rpg64 = ((uint64_t)Rtot + G - 1) / G;
-	const uint32_t rpg = (uint32_t)(rpg64 < rpg_min ? rpg_min : rpg64);
-	if ((uint64_t)blockIdx.x * PECH_GROUPS_PER_WG * rpg >= Rtot)
+	Rtot = uni(Rtot);
+	const uint64_t W = (uint64_t)gridDim.x * PECH_WAVES_PER_WG;
+	const uint64_t rpw64 = ((uint64_t)Rtot + W - 1) / W;
+	const uint32_t rpw = (uint32_t)(rpw64 < rpw_min ? rpw_min : rpw64);
+	if ((uint64_t)blockIdx.x * PECH_WAVES_PER_WG * rpw >= Rtot)
 		return; // whole workgroup idle (small batch)
 
-	// stage the tables: A_128 replicated once per bank, the rest single copy
+	// stage the tables: A_128 once per bank, the rest single copy
 	for (uint32_t j = tid; j < 8192u; j += PECH_WG_THREADS) {
 		const uint32_t A = j << 4;
 		const uint32_t k = ((A >> 16) << 1) | ((A >> 7) & 1u);
 		const uint32_t v = consts[PECH_C_TAB128 + k * 256u + ((A >> 8) & 0xFFu)];
-		*(uint4 *)((char *)lds + A) = make_uint4(v, v, v, v);
+		*(u32x4 *)((char *)lds + A) = (u32x4)(v);
 	}
 	{
-		const uint4 *c4 = (const uint4 *)(consts + PECH_C_TAB4);
-		for (uint32_t j = tid; j < (PECH_C_WORDS - PECH_C_TAB4) / 4u; j += PECH_WG_THREADS)
-			*(uint4 *)((char *)lds + L_TAB4 + 16u * j) = c4[j];
+		const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
+		for (uint32_t j = tid; j < (PECH_C_TAB1 - PECH_C_TAB4) / 4u; j += PECH_WG_THREADS)
+			*(u32x4 *)((char *)lds + L_TAB4 + 16u * j) = c4[j];
 	}
 	__syncthreads();
 
-	const uint32_t lane = tid & 63u, g8 = tid & 7u;
+	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
 	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
-	const uint64_t r0 = ((uint64_t)blockIdx.x * PECH_GROUPS_PER_WG + (tid >> 3)) * rpg;
+	const uint32_t wid = blockIdx.x * PECH_WAVES_PER_WG + uni(tid >> 6);
+	const uint64_t r0 = (uint64_t)wid * rpw;
 	if (r0 >= Rtot)
 		return;
-	uint32_t rem = (uint32_t)(((uint64_t)Rtot - r0) < rpg ? ((uint64_t)Rtot - r0) : rpg);
+	uint32_t rem = uni((uint32_t)min((uint64_t)rpw, (uint64_t)Rtot - r0));
 
-	// locate the first buffer: chunk by binary search in LDS, then an 8-ary
-	// search over the chunk's row offsets with the group's 8 lanes
+	// locate the first buffer: chunk by binary search of the LDS prefix, then
+	// a 64-ary search of the chunk's row offsets (2 rounds for 1024 entries)
 	uint32_t clo = 0, chi = nchunks;
 	while (chi - clo > 1) {
 		const uint32_t mid = (clo + chi) >> 1;
-		if (lds[L_CHUNK / 4u + mid] <= r0)
+		if (uni(lds[L_CHUNK / 4u + mid]) <= r0)
 			clo = mid;
 		else
 			chi = mid;
 	}
-	const uint32_t rr = (uint32_t)(r0 - lds[L_CHUNK / 4u + clo]);
-	uint32_t blo = clo * PECH_CHUNK, bhi = min(n, blo + PECH_CHUNK);
-	while (bhi - blo > 1) {
-		const uint32_t step = (bhi - blo + 7u) >> 3;
-		const uint32_t p = blo + g8 * step;
-		const bool ok = p < bhi && lrs[p] <= rr;
-		const uint64_t bal = __ballot(ok);
-		const uint32_t cnt = __popc((uint32_t)(bal >> (lane & ~7u)) & 0xFFu);
-		blo = blo + (cnt - 1u) * step;
-		bhi = min(bhi, blo + step);
+	const uint32_t rr = uni((uint32_t)(r0 - lds[L_CHUNK / 4u + clo]));
+	uint32_t plo = clo * PECH_CHUNK, phi = plo + uni(lds[L_NZ / 4u + clo]);
+	while (phi - plo > 1) {
+		const uint32_t step = (phi - plo + 63u) >> 6;
+		const uint32_t p = plo + lane * step;
+		const bool ok = p < phi && lrs[p] <= rr;
+		const uint32_t cnt = (uint32_t)__popcll(__ballot(ok));
+		plo = uni(plo + (cnt - 1u) * step);
+		phi = uni(min(phi, plo + step));
 	}
+	uint32_t pos = plo;
+	uint32_t lr = uni(rr - lrs[pos]);
 
-	CompCur C;
-	LoadCur L;
-	{
-		const pech_desc d = load_desc(descs, blo);
-		const uint32_t lr = rr - lrs[blo];
-		const uint32_t rows = pech_rows(d.addr, d.len);
-		const uint64_t a1 = (d.addr + (d.len < 4u ? 4u : d.len) + 15u) & ~(uint64_t)15;
-		const uint64_t vb = a1 - (uint64_t)PECH_ROW_BYTES * rows;
-		C.pa = vb + (uint64_t)PECH_ROW_BYTES * lr + 16u * g8;
-		C.ptr = d.addr;
-		C.len = d.len;
-		C.seed = d.seed;
-		C.lr = lr;
-		C.rows = rows;
-		C.z = (uint32_t)(a1 - (d.addr + d.len));
-		C.b = blo;
-		C.seg0 = lr;
-		C.edge = (((d.addr | (d.addr + d.len)) & 15u) != 0) || d.seed != 0;
-		L.pa = C.pa;
-		L.a0 = d.addr & ~(uint64_t)15;
-		L.left = rows - lr;
-		L.b = blo;
-		if (blo + 1 < n) {
-			L.nd = load_desc(descs, blo + 1);
-			C.nd = L.nd;
-		} else {
-			L.nd = pech_desc{0, 0, 0};
-			C.nd = L.nd;
+	while (rem) {
+		const uint32_t c = pos >> 10;
+		if ((pos & 1023u) >= uni(lds[L_NZ / 4u + c])) {
+			pos = (c + 1u) << 10;
+			continue;
 		}
-	}
-
-	const uint32_t total = rem;
-	u32x4 ring[PECH_PREFETCH];
-	uint32_t issued = 0;
-#pragma unroll
-	for (int i = 0; i < PECH_PREFETCH; ++i) {
-		ring[i] = (u32x4)(0u);
-		if (issued < total) {
-			if (L.pa >= L.a0)
-				ring[i] = *(g_u32x4 *)L.pa;
-			++issued;
-			if (issued < total) {
-				// advance the load cursor one row
-				L.pa += PECH_ROW_BYTES;
-				if (--L.left == 0) {
-					uint32_t b = L.b + 1;
-					pech_desc d = L.nd;
-					while (d.len == 0) {
-						++b;
-						d = load_desc(descs, b);
-					}
-					const uint32_t rows = pech_rows(d.addr, d.len);
-					const uint64_t a1 = (d.addr + (d.len < 4u ? 4u : d.len) + 15u) & ~(uint64_t)15;
-					L.pa = a1 - (uint64_t)PECH_ROW_BYTES * rows + 16u * g8;
-					L.a0 = d.addr & ~(uint64_t)15;
-					L.left = rows;
-					L.b = b;
-					if (b + 1 < n)
-						L.nd = load_desc(descs, b + 1);
-				}
+		const pech_core cd = cores[pos];
+		const uint32_t rows0 = uni(cd.rows);
+		const uint32_t avail0 = rows0 - lr;
+		uint32_t s0, s1, s2, s3;
+		if (avail0 >= PECH_SPLIT_ROWS && rem >= 64u) {
+			// one large buffer (portion): 8 contiguous slices, one per group
+			const uint32_t P = min(avail0, rem);
+			const uint32_t q = P >> 3, rm = P & 7u;
+			const uint32_t st = lr + grp * q + min(grp, rm);
+			const uint32_t nn = q + (grp < rm ? 1u : 0u);
+			const uint64_t ad = uni64(cd.vbase) + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
+			const uint32_t meta = uni(cd.meta);
+			const uint32_t vp = PECH_META_VP(meta);
+			const uint32_t zoff = (st == 0 && g8 < vp) ? 16u * (vp - g8) : 0u;
+			const uint64_t vb = uni64(cd.vbase);
+			run_rows(lds, lreg, ad, nn, nn, zoff, q + (rm ? 1u : 0u), q, s0, s1, s2, s3, vb + 16u * vp,
+				 vb + (uint64_t)rows0 * PECH_ROW_BYTES);
+			const uint64_t m = (uint64_t)(rows0 - st - nn) * PECH_ROW_BYTES + PECH_META_TAIL(meta);
+			finish_run(lds, g8, s0, s1, s2, s3, m, true, out, PECH_META_ORIG(meta));
+			rem -= P;
+			if (P == avail0) {
+				++pos;
+				lr = 0;
+			} else {
+				lr += P;
 			}
-		}
-	}
-
-	uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-	uint32_t done = 0;
-	while (done < total) {
+		} else {
+			// up to 8 neighbouring buffers, one per group
+			const uint32_t nzc = uni(lds[L_NZ / 4u + c]);
+			const uint32_t myp = pos + grp;
+			const bool inchunk = (myp & 1023u) < nzc && (myp >> 10) == c;
+			pech_core my = cd;
+			if (grp && inchunk)
+				my = cores[myp];
+			const uint32_t myrows = inchunk ? my.rows : 0u;
+			// cut at the first non-first group whose buffer is large or out of chunk
+			const bool cut = grp > 0 && (!inchunk || myrows >= PECH_SPLIT_ROWS);
+			const uint64_t cutm = __ballot(cut && g8 == 0);
+			const uint32_t kcut = cutm ? (uint32_t)(__builtin_ctzll(cutm) >> 3) : 8u;
+			const uint32_t mylr = grp ? 0u : lr;
+			const uint32_t avail = grp < kcut ? myrows - mylr : 0u;
+			// exclusive prefix of avail over groups (lanes 8j)
+			uint32_t pre = avail, x;
+			x = __shfl_up(pre, 8);
+			if (lane >= 8)
+				pre += x;
+			x = __shfl_up(pre, 16);
+			if (lane >= 16)
+				pre += x;
+			x = __shfl_up(pre, 32);
+			if (lane >= 32)
+				pre += x;
+			pre -= avail;
+			const uint32_t nu = pre >= rem ? 0u : min(avail, rem - pre);
+			// uniform T = max nu, nmin = min nu over active groups
+			uint32_t tmax = nu, tmin = nu ? nu : 0xFFFFFFFFu;
 #pragma unroll
-		for (int i = 0; i < PECH_PREFETCH; ++i) {
-			if (done < total) {
-				u32x4 w = ring[i];
-				if (issued < total) {
-					u32x4 v = (u32x4)(0u);
-					if (L.pa >= L.a0)
-						v = *(g_u32x4 *)L.pa;
-					ring[i] = v;
-					++issued;
-					if (issued < total) {
-						L.pa += PECH_ROW_BYTES;
-						if (--L.left == 0) {
-							uint32_t b = L.b + 1;
-							pech_desc d = L.nd;
-							while (d.len == 0) {
-								++b;
-								d = load_desc(descs, b);
-							}
-							const uint32_t rows = pech_rows(d.addr, d.len);
-							const uint64_t a1 = (d.addr + (d.len < 4u ? 4u : d.len) + 15u) & ~(uint64_t)15;
-							L.pa = a1 - (uint64_t)PECH_ROW_BYTES * rows + 16u * g8;
-							L.a0 = d.addr & ~(uint64_t)15;
-							L.left = rows;
-							L.b = b;
-							if (b + 1 < n)
-								L.nd = load_desc(descs, b + 1);
-						}
-					}
-				}
-
-				if (C.edge && (C.lr <= 1u || C.lr + 1u == C.rows))
-					w = fix_piece(w, C.pa, C.ptr, C.len, C.seed);
-				s0 = adv128(lds, s0, lreg) ^ w.x;
-				s1 = adv128(lds, s1, lreg) ^ w.y;
-				s2 = adv128(lds, s2, lreg) ^ w.z;
-				s3 = adv128(lds, s3, lreg) ^ w.w;
-				++C.lr;
-				C.pa += PECH_ROW_BYTES;
-				++done;
-
-				if (C.lr == C.rows || done == total) {
-					// fold the 4 streams of the lane, then the 8 lanes of the row
-					uint32_t u = adv_tab(lds, L_TAB4, s0) ^ s1;
-					u = adv_tab(lds, L_TAB4, u) ^ s2;
-					u = adv_tab(lds, L_TAB4, u) ^ s3;
-					u = adv_tab(lds, L_TAB4, u);
-					uint32_t o, lo, hi;
-					o = __shfl_xor(u, 1);
-					lo = (g8 & 1u) ? o : u;
-					hi = (g8 & 1u) ? u : o;
-					u = adv_tab(lds, L_TAB16, lo) ^ hi;
-					o = __shfl_xor(u, 2);
-					lo = (g8 & 2u) ? o : u;
-					hi = (g8 & 2u) ? u : o;
-					u = adv_tab(lds, L_TAB32, lo) ^ hi;
-					o = __shfl_xor(u, 4);
-					lo = (g8 & 4u) ? o : u;
-					hi = (g8 & 4u) ? u : o;
-					u = adv_tab(lds, L_TAB64, lo) ^ hi;
-					// shift to the buffer's end, undo the z trailing zeros
-					const uint32_t k = C.rows - C.lr;
-					if (C.z)
-						u = gf2_mulmod(lds[L_XINV / 4u + C.z], u);
-#pragma unroll
-					for (uint32_t i6 = 0; i6 < 5; ++i6) {
-						const uint32_t dg = (k >> (6u * i6)) & 63u;
-						if (dg)
-							u = gf2_mulmod(lds[L_POWR / 4u + 64u * i6 + dg], u);
-					}
-					if (g8 == 0) {
-						if (C.seg0 == 0 && k == 0)
-							out[C.b] = u;
-						else
-							atomicXor(out + C.b, u);
-					}
-					s0 = s1 = s2 = s3 = 0;
-					if (done < total) {
-						// next buffer
-						uint32_t b = C.b + 1;
-						pech_desc d = C.nd;
-						while (d.len == 0) {
-							++b;
-							d = load_desc(descs, b);
-						}
-						const uint32_t rows = pech_rows(d.addr, d.len);
-						const uint64_t a1 = (d.addr + (d.len < 4u ? 4u : d.len) + 15u) & ~(uint64_t)15;
-						C.pa = a1 - (uint64_t)PECH_ROW_BYTES * rows + 16u * g8;
-						C.ptr = d.addr;
-						C.len = d.len;
-						C.seed = d.seed;
-						C.lr = 0;
-						C.rows = rows;
-						C.z = (uint32_t)(a1 - (d.addr + d.len));
-						C.b = b;
-						C.seg0 = 0;
-						C.edge = (((d.addr | (d.addr + d.len)) & 15u) != 0) || d.seed != 0;
-						if (b + 1 < n)
-							C.nd = load_desc(descs, b + 1);
-					}
-				}
+			for (uint32_t d = 8; d < 64; d <<= 1) {
+				tmax = max(tmax, (uint32_t)__shfl_xor(tmax, d));
+				tmin = min(tmin, (uint32_t)__shfl_xor(tmin, d));
+			}
+			const uint32_t T = uni(tmax), nmin = uni(tmin);
+			const uint32_t used = uni(min((uint32_t)__shfl(pre + avail, 63), rem));
+			// idle groups reload group 0's rows (valid memory), state ignored
+			const uint64_t ad0 = uni64(cd.vbase) + (uint64_t)lr * PECH_ROW_BYTES + 16u * g8;
+			const uint32_t vp0 = PECH_META_VP(uni(cd.meta));
+			const uint32_t z0 = (lr == 0 && g8 < vp0) ? 16u * (vp0 - g8) : 0u;
+			const uint32_t n0 = min(avail0, rem);
+			const uint32_t myvp = PECH_META_VP(my.meta);
+			const uint32_t zm = (mylr == 0 && g8 < myvp) ? 16u * (myvp - g8) : 0u;
+			const uint64_t ad = nu ? my.vbase + (uint64_t)mylr * PECH_ROW_BYTES + 16u * g8 : ad0;
+			const uint64_t bv = nu ? my.vbase : uni64(cd.vbase);
+			const uint32_t bvp = nu ? myvp : vp0, brows = nu ? myrows : rows0;
+			run_rows(lds, lreg, ad, nu ? nu : n0, nu, nu ? zm : z0, T, nmin, s0, s1, s2, s3, bv + 16u * bvp,
+				 bv + (uint64_t)brows * PECH_ROW_BYTES);
+			const uint64_t m = (uint64_t)(myrows - mylr - nu) * PECH_ROW_BYTES + PECH_META_TAIL(my.meta);
+			finish_run(lds, g8, s0, s1, s2, s3, m, nu != 0, out, PECH_META_ORIG(my.meta));
+			rem -= used;
+			if (rem) { // then every group < kcut finished its buffer
+				pos += kcut;
+				lr = 0;
 			}
 		}
 	}
 }
 
 // ---- host-side launchers (used by crc32c_api.cpp) -------------------------
-extern "C" hipError_t pech_launch_plan(const pech_desc *descs, uint32_t n, uint32_t *lrs, uint32_t *partials,
-				       uint32_t *out, hipStream_t stream)
+extern "C" hipError_t pech_launch_plan(const pech_desc *descs, uint32_t n, pech_core *cores, uint32_t *lrs,
+				       uint32_t *partials, uint32_t *nzs, const uint32_t *consts, uint32_t *out,
+				       hipStream_t stream)
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
-	hipLaunchKernelGGL(pech_crc32c_plan, dim3(nch), dim3(PECH_WG_THREADS), 0, stream, descs, n, lrs, partials,
-			   out);
+	hipLaunchKernelGGL(pech_crc32c_plan, dim3(nch), dim3(PECH_WG_THREADS), 0, stream, descs, n, cores, lrs,
+			   partials, nzs, consts, out);
 	return hipGetLastError();
 }
 
-extern "C" hipError_t pech_launch_main(const pech_desc *descs, uint32_t n, const uint32_t *lrs,
-				       const uint32_t *partials, const uint32_t *consts, uint32_t *out,
-				       uint32_t ncu, uint32_t rpg_min, hipStream_t stream)
+extern "C" hipError_t pech_launch_main(const pech_core *cores, uint32_t n, const uint32_t *lrs,
+				       const uint32_t *partials, const uint32_t *nzs, const uint32_t *consts,
+				       uint32_t *out, uint32_t ncu, uint32_t rpw_min, hipStream_t stream)
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
-	hipLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_WG_THREADS), 0, stream, descs, n, lrs, partials,
-			   nch, consts, out, rpg_min);
+	hipLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_WG_THREADS), 0, stream, cores, lrs, partials, nzs,
+			   nch, consts, out, rpw_min);
 	return hipGetLastError();
+}
+
+#define PECH_STR2(x) #x
+#define PECH_STR(x) PECH_STR2(x)
+extern "C" const char *pech_kernel_tag(void)
+{
+	return "pech_crc32c 0.2 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(PECH_U);
 }

@@ -1,18 +1,22 @@
 /*
  * layout.h -- geometry shared by the host library and the gfx950 kernels.
  *
- * Virtual row space.  Every buffer (addr, len) is viewed as a run of 16-byte
- * aligned "pieces" [a0, a1), a0 = addr & ~15, a1 = align16(addr + max(len,4)),
- * grouped into 128-byte "rows" (8 pieces, one HBM cache line) that are
- * RIGHT-aligned to a1.  Pieces of the first row that lie below a0 are
- * virtual zeros (leading zeros do not change R(0, .)); bytes of real pieces
- * outside [addr, addr+len) are masked to zero; the z = a1 - (addr+len)
- * trailing zeros are undone by a final multiply with x^(-8z).  The seed is
- * xored into bytes [addr, addr+4) (gf2.h identities).
+ * Split of one buffer D = (addr, len, seed) (gf2.h identities):
+ *   head h = [addr, cs)        cs = align16(addr)              (< 16 bytes)
+ *   core c = [cs, ce)          ce = align16_down(addr + len)   (16-byte pieces)
+ *   tail t = [ce, addr + len)                                  (< 16 bytes)
+ *   crc32c(seed, D) = x^(8|t|) * R(0, c)                      <- main kernel
+ *                   ^ x^(8 len) * seed
+ *                   ^ x^(8(|c|+|t|)) * R(0, h) ^ R(0, t)      <- plan kernel
+ * Buffers with no full aligned piece (len < 16 or spanning < one aligned
+ * 16-byte block) are checksummed entirely by the plan kernel (<= 30 bytes).
  *
- * One 8-lane "group" of a wave owns a contiguous range of rows of the
- * concatenated row space of a batch; lane g8 of the group holds piece g8 of
- * each row as four 4-byte "streams".
+ * Row space.  The core's 16-byte pieces are grouped in 128-byte ROWS (8
+ * pieces = one HBM cache line), right-aligned to ce: row 0 starts at
+ * vbase = ce - 128*rows and its first vp pieces (vp < 8) are virtual zeros
+ * (leading zeros do not change R(0, .)).  One 8-lane GROUP of a wave walks
+ * rows of one buffer; lane g8 of the group holds piece g8 of every row as
+ * four 4-byte register "streams".
  */
 #ifndef PECH_CRC32C_LAYOUT_H
 #define PECH_CRC32C_LAYOUT_H
@@ -23,21 +27,23 @@
 #define PECH_PIECE_BYTES 16u
 #define PECH_GROUP_LANES 8u
 #define PECH_WG_THREADS 1024u
-#define PECH_GROUPS_PER_WG (PECH_WG_THREADS / PECH_GROUP_LANES)
+#define PECH_WAVES_PER_WG (PECH_WG_THREADS / 64u)
 #define PECH_CHUNK 1024u          /* buffers per plan chunk (one plan WG)  */
 #define PECH_MAX_CHUNKS 1024u     /* => at most 2^20 buffers per launch    */
 #define PECH_MAX_BATCH (PECH_CHUNK * PECH_MAX_CHUNKS)
-#define PECH_RPG_MIN 32u          /* min rows per group (4 KiB)            */
+#define PECH_RPW_MIN 64u          /* min rows per wave (8 KiB)             */
+#define PECH_LARGE_ROWS 2048u     /* size-class cap for the plan's ordering  */
+#define PECH_SPLIT_ROWS 256u      /* >= this: a buffer is split over 8 groups */
 
 /* constants block (u32 words), built on the host, uploaded once per device */
-#define PECH_C_TAB128 0u    /* A_128 byte tables, 4 x 256  (Horner step)   */
-#define PECH_C_TAB4 1024u   /* A_4   byte tables           (lane combine)  */
-#define PECH_C_TAB16 2048u  /* A_16                        (butterfly 1)   */
-#define PECH_C_TAB32 3072u  /* A_32                        (butterfly 2)   */
-#define PECH_C_TAB64 4096u  /* A_64                        (butterfly 3)   */
-#define PECH_C_POWR 5120u   /* x^(1024*j*64^i), i<5, j<64  (row shifts)    */
-#define PECH_C_XINV 5440u   /* x^(-8z), z<32               (tail undo)     */
-#define PECH_C_WORDS 5472u
+#define PECH_C_TAB128 0u    /* A_128 byte tables, 4 x 256  (row Horner step)  */
+#define PECH_C_TAB4 1024u   /* A_4   byte tables           (lane fold)        */
+#define PECH_C_TAB16 2048u  /* A_16                        (butterfly 1)      */
+#define PECH_C_TAB32 3072u  /* A_32                        (butterfly 2)      */
+#define PECH_C_TAB64 4096u  /* A_64                        (butterfly 3)      */
+#define PECH_C_POWB 5120u   /* x^(8*j*64^i), i<6, j<64     (byte shifts)      */
+#define PECH_C_TAB1 5504u   /* A_1 = the reference table, include/crc32c.h:16 */
+#define PECH_C_WORDS 5760u
 
 /* device batch descriptor (matches struct crc32c_desc in include/) */
 struct pech_desc {
@@ -46,22 +52,46 @@ struct pech_desc {
 	uint32_t seed;
 };
 
+/* per-buffer core descriptor written by the plan kernel, in row-space order */
+struct pech_core {
+	uint64_t vbase; /* address of row 0, piece 0 (may precede the core)      */
+	uint32_t rows;  /* rows of the core (0: buffer fully done by the plan)   */
+	uint32_t meta;  /* orig index (bits 0-19) | vp (20-22) | tail (24-27)    */
+};
+
+#define PECH_META(orig, vp, t) ((orig) | ((uint32_t)(vp) << 20) | ((uint32_t)(t) << 24))
+#define PECH_META_ORIG(m) ((m) & 0xFFFFFu)
+#define PECH_META_VP(m) (((m) >> 20) & 7u)
+#define PECH_META_TAIL(m) (((m) >> 24) & 15u)
+
 #ifdef __HIPCC__
 #define LAYOUT_FN __host__ __device__ inline
 #else
 #define LAYOUT_FN static inline
 #endif
 
-/* rows of buffer (addr, len) in the virtual row space; 0 for len == 0 */
-LAYOUT_FN uint32_t pech_rows(uint64_t addr, uint32_t len)
+/* rows of the core of buffer (addr, len); 0 if it has no full aligned piece */
+LAYOUT_FN uint32_t pech_core_rows(uint64_t addr, uint32_t len)
 {
-	if (len == 0)
+	const uint64_t cs = (addr + 15) & ~(uint64_t)15;
+	const uint64_t ce = (addr + len) & ~(uint64_t)15;
+	if (ce <= cs)
 		return 0;
-	uint64_t a0 = addr & ~(uint64_t)15;
-	uint64_t e4 = addr + (len < 4 ? 4u : len);
-	uint64_t a1 = (e4 + 15) & ~(uint64_t)15;
-	uint32_t pieces = (uint32_t)((a1 - a0) >> 4);
+	const uint32_t pieces = (uint32_t)((ce - cs) >> 4);
 	return (pieces + 7) >> 3;
 }
+
+/* size class used to order buffers inside a plan chunk (similar row counts
+ * become neighbours, so the 8 groups of a wave get similar work) */
+LAYOUT_FN uint32_t pech_size_class(uint32_t rows)
+{
+	if (rows >= PECH_LARGE_ROWS)
+		return 12;
+	uint32_t c = 0;
+	while ((2u << c) <= rows)
+		++c;
+	return c; /* floor(log2(rows)), 0..10 */
+}
+#define PECH_NCLASS 13u
 
 #endif /* PECH_CRC32C_LAYOUT_H */

@@ -1,0 +1,228 @@
+"""Host-side shadow model of the work decomposition of
+pech_amd/csrc/crc32c_kernels.hip (plan + main kernels), statement by
+statement, used by tests/test_kernel_model.py to check -- on the CPU, before a
+kernel ever runs on a GPU -- that
+
+  * every 16-byte load the main kernel issues lies inside the real core of
+    the buffer it is working on (no read before/after a buffer: a GPU fault),
+  * every core row of every buffer is consumed by exactly one lane-group,
+  * every run's final shift targets the right buffer end.
+
+Keep in sync with the kernel: constants come from layout.h by parsing.
+"""
+import os
+import re
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _consts():
+    src = open(os.path.join(REPO, "pech_amd", "csrc", "layout.h")).read()
+    out = {}
+    for m in re.finditer(r"#define (PECH_\w+) (\d+)u", src):
+        out[m.group(1)] = int(m.group(2))
+    ksrc = open(os.path.join(REPO, "pech_amd", "csrc", "crc32c_kernels.hip")).read()
+    out["PECH_U"] = int(re.search(r"#define PECH_U (\d+)", ksrc).group(1))
+    return out
+
+
+C = _consts()
+ROW = C["PECH_ROW_BYTES"]
+CHUNK = C["PECH_CHUNK"]
+SPLIT = C["PECH_SPLIT_ROWS"]
+LARGE = C["PECH_LARGE_ROWS"]
+WAVES_PER_WG = C["PECH_WG_THREADS"] // 64
+
+
+def core_rows(addr, ln):
+    cs = (addr + 15) & ~15
+    ce = (addr + ln) & ~15
+    if ce <= cs:
+        return 0
+    return (((ce - cs) >> 4) + 7) >> 3
+
+
+def size_class(rows):
+    if rows >= LARGE:
+        return 12
+    c = 0
+    while (2 << c) <= rows:
+        c += 1
+    return c
+
+
+def plan(descs, rng=None):
+    """descs: list of (addr, len).  Returns per-slot cores, lrs, partials,
+    nzs.  Order inside a size class is arbitrary on the GPU (LDS atomics);
+    `rng` shuffles it to cover that."""
+    n = len(descs)
+    nch = (n + CHUNK - 1) // CHUNK
+    cores = [None] * (nch * CHUNK)
+    lrs = [0] * (nch * CHUNK)
+    partials, nzs = [], []
+    for c in range(nch):
+        items = []
+        for b in range(c * CHUNK, min(n, (c + 1) * CHUNK)):
+            addr, ln = descs[b]
+            rows = core_rows(addr, ln)
+            if rows == 0:
+                continue
+            cs = (addr + 15) & ~15
+            ce = (addr + ln) & ~15
+            vp = rows * 8 - ((ce - cs) >> 4)
+            t = addr + ln - ce
+            items.append(dict(vbase=ce - ROW * rows, rows=rows, orig=b, vp=vp, tail=t, cs=cs, ce=ce,
+                              cls=size_class(rows)))
+        order = []
+        for cls in range(13):
+            group = [it for it in items if it["cls"] == cls]
+            if rng is not None:
+                rng.shuffle(group)
+            order += group
+        acc = 0
+        for pos in range(CHUNK):
+            lrs[c * CHUNK + pos] = acc
+            if pos < len(order):
+                cores[c * CHUNK + pos] = order[pos]
+                acc += order[pos]["rows"]
+        partials.append(acc)
+        nzs.append(len(order))
+    return cores, lrs, partials, nzs
+
+
+def run_rows_loads(U, nl, nu, zoff, T, nmin):
+    """Row indices (and whether the zoff redirect applies) loaded by
+    run_rows for one lane, and the rows it consumes (r < nu)."""
+    last = nl - 1
+    loads = []
+
+    def row_addr(row):
+        loads.append((row, row == 0 and zoff != 0))
+
+    for i in range(U):
+        row_addr(min(i, last))
+    nblk = (T + U - 1) // U
+    blk = 0
+    while blk + 1 < nblk and (blk + 2) * U <= nmin:
+        for i in range(U):
+            loads.append(((blk + 1) * U + i, False))
+        blk += 1
+    while blk + 1 < nblk:
+        r = blk * U
+        for i in range(U):
+            row_addr(min(r + U + i, last))
+        blk += 1
+    consumed = [r for r in range(nblk * U) if r < nu]
+    return loads, consumed
+
+
+def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None):
+    """Yield events: ("load", buf, lane_piece_addr) and ("use", orig, row,
+    g8) and ("finish", orig, group_end_row, m)."""
+    U = U or C["PECH_U"]
+    rpw_min = rpw_min or C["PECH_RPW_MIN"]
+    nchunks = len(partials)
+    pref = [0]
+    for p in partials:
+        pref.append(pref[-1] + p)
+    Rtot = pref[-1]
+    W = ncu * WAVES_PER_WG
+    rpw = max(rpw_min, (Rtot + W - 1) // W)
+    events = []
+    for wid in range(W):
+        r0 = wid * rpw
+        if r0 >= Rtot:
+            continue
+        rem = min(rpw, Rtot - r0)
+        # chunk search: largest c with pref[c] <= r0
+        clo, chi = 0, nchunks
+        while chi - clo > 1:
+            mid = (clo + chi) >> 1
+            if pref[mid] <= r0:
+                clo = mid
+            else:
+                chi = mid
+        rr = r0 - pref[clo]
+        plo, phi = clo * CHUNK, clo * CHUNK + nzs[clo]
+        while phi - plo > 1:
+            step = (phi - plo + 63) >> 6
+            cnt = sum(1 for lane in range(64) if plo + lane * step < phi and lrs[plo + lane * step] <= rr)
+            plo = plo + (cnt - 1) * step
+            phi = min(phi, plo + step)
+        pos = plo
+        lr = rr - lrs[pos]
+        guard = 0
+        while rem:
+            guard += 1
+            assert guard < 10 ** 6, "wave loop does not terminate"
+            c = pos >> 10
+            if (pos & 1023) >= nzs[c]:
+                pos = (c + 1) << 10
+                continue
+            cd = cores[pos]
+            rows0 = cd["rows"]
+            avail0 = rows0 - lr
+            assert avail0 > 0
+            if avail0 >= SPLIT and rem >= 64:
+                P = min(avail0, rem)
+                q, rm = P >> 3, P & 7
+                T = q + (1 if rm else 0)
+                for grp in range(8):
+                    st = lr + grp * q + min(grp, rm)
+                    nn = q + (1 if grp < rm else 0)
+                    for g8 in range(8):
+                        zoff = 16 * (cd["vp"] - g8) if (st == 0 and g8 < cd["vp"]) else 0
+                        loads, used = run_rows_loads(U, nn, nn, zoff, T, q)
+                        for row, z in loads:
+                            events.append(("load", cd, cd["vbase"] + (st + row) * ROW + 16 * g8 + (zoff if z else 0)))
+                        for row in used:
+                            events.append(("use", cd["orig"], st + row, g8, zoff != 0 and row == 0))
+                    events.append(("finish", cd["orig"], st + nn, (rows0 - st - nn) * ROW + cd["tail"]))
+                rem -= P
+                if P == avail0:
+                    pos += 1
+                    lr = 0
+                else:
+                    lr += P
+            else:
+                nzc = nzs[c]
+                mys, cut = [], []
+                for grp in range(8):
+                    myp = pos + grp
+                    inchunk = (myp & 1023) < nzc and (myp >> 10) == c
+                    my = cores[myp] if (grp and inchunk) else cd
+                    myrows = my["rows"] if inchunk else 0
+                    cut.append(grp > 0 and (not inchunk or myrows >= SPLIT))
+                    mys.append((my, myrows))
+                kcut = next((g for g in range(8) if cut[g]), 8)
+                avails = [(mys[g][1] - (lr if g == 0 else 0)) if g < kcut else 0 for g in range(8)]
+                pres = [sum(avails[:g]) for g in range(8)]
+                nus = [0 if pres[g] >= rem else min(avails[g], rem - pres[g]) for g in range(8)]
+                T = max(nus)
+                nmin = min(x for x in nus if x) if any(nus) else 0xFFFFFFFF
+                used_rows = min(pres[7] + avails[7], rem)
+                assert used_rows == sum(nus)
+                n0 = min(avail0, rem)
+                for grp in range(8):
+                    my, myrows = mys[grp]
+                    nu = nus[grp]
+                    mylr = 0 if grp else lr
+                    for g8 in range(8):
+                        if nu:
+                            zoff = 16 * (my["vp"] - g8) if (mylr == 0 and g8 < my["vp"]) else 0
+                            base, buf, nl = my["vbase"] + mylr * ROW + 16 * g8, my, nu
+                        else:
+                            zoff = 16 * (cd["vp"] - g8) if (lr == 0 and g8 < cd["vp"]) else 0
+                            base, buf, nl = cd["vbase"] + lr * ROW + 16 * g8, cd, n0
+                        loads, used = run_rows_loads(U, nl, nu, zoff, T, nmin)
+                        for row, z in loads:
+                            events.append(("load", buf, base + row * ROW + (zoff if z else 0)))
+                        for row in used:
+                            events.append(("use", my["orig"], mylr + row, g8, zoff != 0 and row == 0))
+                    if nu:
+                        events.append(("finish", my["orig"], mylr + nu, (myrows - mylr - nu) * ROW + my["tail"]))
+                rem -= used_rows
+                if rem:
+                    pos += kcut
+                    lr = 0
+    return events

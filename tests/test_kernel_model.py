@@ -1,0 +1,81 @@
+"""CPU checks of the main kernel's work decomposition through the shadow
+model (tests/kernel_model.py): loads stay inside real buffer cores, every
+core row is consumed exactly once, shifts target the buffer end."""
+import collections
+import random
+
+import pytest
+
+import kernel_model as KM
+
+
+def check(descs, ncu=4, seed=0):
+    rng = random.Random(seed)
+    cores, lrs, partials, nzs = KM.plan(descs, rng)
+    ev = KM.main(cores, lrs, partials, nzs, ncu)
+    used = collections.Counter()
+    byorig = {}
+    for c in cores:
+        if c is not None:
+            byorig[c["orig"]] = c
+    for e in ev:
+        if e[0] == "load":
+            _, buf, a = e
+            assert buf["cs"] <= a and a + 16 <= buf["ce"], (buf, a)
+        elif e[0] == "use":
+            _, orig, row, g8, virt = e
+            c = byorig[orig]
+            used[(orig, row, g8)] += 1
+            piece = row * 8 + g8
+            assert virt == (piece < c["vp"]), (orig, row, g8)
+        elif e[0] == "finish":
+            _, orig, endrow, m = e
+            c = byorig[orig]
+            assert m == (c["rows"] - endrow) * KM.ROW + c["tail"]
+    for orig, c in byorig.items():
+        for row in range(c["rows"]):
+            for g8 in range(8):
+                assert used[(orig, row, g8)] == 1, (orig, row, g8, used[(orig, row, g8)])
+    assert sum(used.values()) == 8 * sum(c["rows"] for c in byorig.values())
+
+
+def test_uniform_4k():
+    check([(0x10000 + 4096 * i, 4096) for i in range(300)])
+
+
+def test_uniform_4m_like():
+    # 4 MiB-style large buffers, fewer of them (model cost)
+    check([(0x100000 * (i + 1), 300000) for i in range(6)], ncu=2)
+
+
+def test_tiny_and_unaligned():
+    rng = random.Random(1)
+    descs = []
+    base = 1 << 20
+    for i in range(500):
+        ln = rng.choice([0, 1, 5, 15, 16, 17, 31, 32, 33, 64, 100, 127, 128, 129, 1000, 4095, 4097, 20000])
+        off = rng.randrange(0, 64)
+        descs.append((base + off, ln))
+        base += off + ln + rng.randrange(0, 32)
+    check(descs, ncu=3)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_mixed_sizes(seed):
+    rng = random.Random(seed)
+    sizes = [4096] * 200 + [65536] * 20 + [300000] * 3 + [16] * 30 + [7] * 10
+    rng.shuffle(sizes)
+    descs, base = [], 4096
+    for s in sizes:
+        descs.append((base, s))
+        base += s
+    check(descs, ncu=2, seed=seed)
+
+
+def test_many_chunks_and_empty_chunks():
+    descs = [(4096 * (i + 1), 0 if (i // 1024) == 1 else 256) for i in range(3000)]
+    check(descs, ncu=1)
+
+
+def test_one_buffer_many_waves():
+    check([(1 << 30, 4 << 20)], ncu=1)

@@ -1,0 +1,154 @@
+// hbm_probe.hip -- read-bandwidth probes on the GPU box (not product code).
+// Measures what HBM read rate different access shapes reach on MI355X, as
+// context for the CRC kernel's roofline:
+//   stream   : grid-stride, every wave reads contiguous 1 KiB per instruction
+//   groupG   : the CRC kernel's shape -- G-lane groups, each walking its own
+//              contiguous range in (G*16)-byte rows, D rows in flight per lane
+// Build: hipcc -O3 --offload-arch=gfx950 tools/hbm_probe.hip -o build/hbm_probe
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+
+#define CHECK(x)                                                                   \
+	do {                                                                       \
+		hipError_t e = (x);                                                \
+		if (e != hipSuccess) {                                             \
+			fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));     \
+			exit(1);                                                   \
+		}                                                                  \
+	} while (0)
+
+template <int UNROLL>
+__global__ __launch_bounds__(1024) void k_stream(const u32x4 *p, size_t n16, uint32_t *out)
+{
+	const size_t tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+	const size_t stride = (size_t)gridDim.x * blockDim.x;
+	u32x4 acc = (u32x4)(0u);
+	size_t i = tid;
+	for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
+		u32x4 v[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; ++u)
+			v[u] = *(g_u32x4 *)(p + i + u * stride);
+#pragma unroll
+		for (int u = 0; u < UNROLL; ++u)
+			acc ^= v[u];
+	}
+	for (; i < n16; i += stride)
+		acc ^= *(g_u32x4 *)(p + i);
+	const uint32_t r = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (r == 0x12345678u)
+		out[tid] = r;
+}
+
+// G lanes per group, each group a contiguous range of `rows` rows of G*16 B
+template <int G, int D>
+__global__ __launch_bounds__(1024) void k_group(const uint8_t *p, uint32_t rows_per_group, uint32_t *out)
+{
+	const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+	const uint32_t gl = threadIdx.x % G;
+	const uint8_t *base = p + (size_t)gid * rows_per_group * (G * 16) + gl * 16;
+	u32x4 acc = (u32x4)(0u);
+	u32x4 ring[D];
+#pragma unroll
+	for (int d = 0; d < D; ++d)
+		ring[d] = *(g_u32x4 *)(base + (size_t)d * G * 16);
+	uint32_t r = D;
+	for (; r + D <= rows_per_group; r += D) {
+#pragma unroll
+		for (int d = 0; d < D; ++d) {
+			acc ^= ring[d];
+			ring[d] = *(g_u32x4 *)(base + (size_t)(r + d) * G * 16);
+		}
+	}
+#pragma unroll
+	for (int d = 0; d < D; ++d)
+		acc ^= ring[d];
+	for (; r < rows_per_group; ++r)
+		acc ^= *(g_u32x4 *)(base + (size_t)r * G * 16);
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[gid] = x;
+}
+
+static float time_it(void (*launch)(void *), void *arg, int reps)
+{
+	hipEvent_t a, b;
+	CHECK(hipEventCreate(&a));
+	CHECK(hipEventCreate(&b));
+	launch(arg);
+	CHECK(hipDeviceSynchronize());
+	CHECK(hipEventRecord(a));
+	for (int i = 0; i < reps; ++i)
+		launch(arg);
+	CHECK(hipEventRecord(b));
+	CHECK(hipEventSynchronize(b));
+	float ms;
+	CHECK(hipEventElapsedTime(&ms, a, b));
+	return ms / reps;
+}
+
+struct Args {
+	uint8_t *buf[2];
+	size_t bytes;
+	uint32_t *out;
+	int ncu;
+	int it;
+};
+
+template <int U> static void launch_stream(void *v)
+{
+	Args *a = (Args *)v;
+	const uint8_t *p = a->buf[a->it++ & 1];
+	hipLaunchKernelGGL(k_stream<U>, dim3(a->ncu * 4), dim3(1024), 0, 0, (const u32x4 *)p, a->bytes / 16, a->out);
+}
+
+template <int G, int D> static void launch_group(void *v)
+{
+	Args *a = (Args *)v;
+	const uint8_t *p = a->buf[a->it++ & 1];
+	const uint32_t groups = a->ncu * 1024 / G;
+	const uint32_t rpg = (uint32_t)(a->bytes / (G * 16) / groups);
+	hipLaunchKernelGGL((k_group<G, D>), dim3(a->ncu), dim3(1024), 0, 0, p, rpg, a->out);
+}
+
+int main(int argc, char **argv)
+{
+	Args a;
+	a.bytes = (size_t)1 << 30;
+	hipDeviceProp_t prop;
+	CHECK(hipGetDeviceProperties(&prop, 0));
+	a.ncu = prop.multiProcessorCount;
+	a.it = 0;
+	for (int i = 0; i < 2; ++i) {
+		CHECK(hipMalloc(&a.buf[i], a.bytes));
+		CHECK(hipMemset(a.buf[i], i + 1, a.bytes));
+	}
+	CHECK(hipMalloc(&a.out, (size_t)a.ncu * 4096 * 4));
+	const int reps = 20;
+	struct {
+		const char *name;
+		void (*fn)(void *);
+	} probes[] = {
+		{"stream u4 (grid 4/CU)", launch_stream<4>},
+		{"stream u8 (grid 4/CU)", launch_stream<8>},
+		{"group8  D4", launch_group<8, 4>},
+		{"group8  D8", launch_group<8, 8>},
+		{"group16 D4", launch_group<16, 4>},
+		{"group32 D4", launch_group<32, 4>},
+		{"group64 D4", launch_group<64, 4>},
+		{"group64 D8", launch_group<64, 8>},
+	};
+	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, a.ncu, a.bytes);
+	for (size_t i = 0; i < sizeof(probes) / sizeof(probes[0]); ++i) {
+		const float ms = time_it(probes[i].fn, &a, reps);
+		printf("  {\"probe\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}%s\n", probes[i].name, ms * 1e3,
+		       a.bytes / (ms * 1e-3) / 1e9, i + 1 < sizeof(probes) / sizeof(probes[0]) ? "," : "");
+	}
+	printf("]}\n");
+	return 0;
+}
