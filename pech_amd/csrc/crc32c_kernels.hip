@@ -67,7 +67,7 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v)
 }
 
 // 1024-thread exclusive scan; scratch = 16 LDS words
-__device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t *total)
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t *total)
 {
 	const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
 	uint32_t x = v;
@@ -101,6 +101,9 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_o
 // Table k, entry e, bank copy c lives at (k>>1)*64K + e*256 + (k&1)*128 + 4c.
 __device__ __forceinline__ uint32_t adv128(const uint32_t *lds, uint32_t s, uint32_t lreg)
 {
+#ifdef PECH_AB_NOLDS // diagnostic build only: no table lookups (wrong CRCs)
+	return (s << 1) ^ (s >> 3) ^ lreg;
+#endif
 	const uint32_t a0 = __builtin_amdgcn_perm(s, lreg, 0x0C0C0400u);
 	const uint32_t a1 = __builtin_amdgcn_perm(s, lreg, 0x0C0C0500u);
 	const uint32_t a2 = __builtin_amdgcn_perm(s, lreg, 0x0C020600u);
@@ -116,7 +119,7 @@ __device__ __forceinline__ uint32_t adv_tab(const uint32_t *lds, uint32_t tab, u
 }
 
 // v * x^(8m) mod P with the 64-ary power table POWB[i][j] = x^(8 j 64^i)
-__device__ inline uint32_t shift_bytes(const uint32_t *powb, uint64_t m, uint32_t v)
+__device__ __forceinline__ uint32_t shift_bytes(const uint32_t *powb, uint64_t m, uint32_t v)
 {
 #pragma unroll
 	for (uint32_t i = 0; i < 6; ++i) {
@@ -129,7 +132,7 @@ __device__ inline uint32_t shift_bytes(const uint32_t *powb, uint64_t m, uint32_
 
 // ---- plan kernel ----------------------------------------------------------
 // byte-wise reference update (include/crc32c.h:92-93) on the LDS table
-__device__ inline uint32_t crc_bytes(const uint32_t *t1, uint32_t crc, uint64_t addr, uint32_t n)
+__device__ __forceinline__ uint32_t crc_bytes(const uint32_t *t1, uint32_t crc, uint64_t addr, uint32_t n)
 {
 	const g_u8 *q = (const g_u8 *)addr;
 	for (uint32_t i = 0; i < n; ++i)
@@ -242,6 +245,8 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 	return *(g_u32x4 *)a;
 }
 #define LD_PIECE(a, tag) ld_piece((a), blo, bhi, (tag))
+#elif defined(PECH_AB_NOLOAD) // diagnostic build only: no HBM reads (wrong CRCs)
+#define LD_PIECE(a, tag) ((u32x4)((uint32_t)(a)))
 #else
 #define LD_PIECE(a, tag) (*(g_u32x4 *)(a))
 #endif
@@ -402,12 +407,24 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 		const uint32_t step = (phi - plo + 63u) >> 6;
 		const uint32_t p = plo + lane * step;
 		const bool ok = p < phi && lrs[p] <= rr;
-		const uint32_t cnt = (uint32_t)__popcll(__ballot(ok));
+		const uint64_t bal = __ballot(ok);
+		const uint32_t cnt = (uint32_t)__popcll(bal);
+#ifdef PECH_DEBUG_BOUNDS
+		if (blockIdx.x == 0 && wid == 3 && p < phi && (lane < 3 || (lane + 3 >= cnt && lane <= cnt + 1)))
+			printf("PECH TRACE search plo %u phi %u step %u lane %u p %u lrs %u ok %d bal %llx cnt %u\n", plo, phi,
+			       step, lane, p, lrs[p], (int)ok, (unsigned long long)bal, cnt);
+#endif
 		plo = uni(plo + (cnt - 1u) * step);
 		phi = uni(min(phi, plo + step));
 	}
 	uint32_t pos = plo;
 	uint32_t lr = uni(rr - lrs[pos]);
+#ifdef PECH_DEBUG_BOUNDS
+	const bool trace = blockIdx.x == 0 && wid == 3 && lane == 0;
+	if (trace)
+		printf("PECH TRACE wid %u r0 %llu rem %u Rtot %u rpw %u clo %u rr %u pos %u lrs[pos] %u lr %u nz %u\n", wid,
+		       (unsigned long long)r0, rem, Rtot, rpw, clo, rr, pos, lrs[pos], lr, lds[L_NZ / 4u + clo]);
+#endif
 
 	while (rem) {
 		const uint32_t c = pos >> 10;
@@ -418,6 +435,10 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 		const pech_core cd = cores[pos];
 		const uint32_t rows0 = uni(cd.rows);
 		const uint32_t avail0 = rows0 - lr;
+#ifdef PECH_DEBUG_BOUNDS
+		if (trace)
+			printf("PECH TRACE step pos %u lr %u rem %u rows0 %u\n", pos, lr, rem, rows0);
+#endif
 		uint32_t s0, s1, s2, s3;
 		if (avail0 >= PECH_SPLIT_ROWS && rem >= 64u) {
 			// one large buffer (portion): 8 contiguous slices, one per group

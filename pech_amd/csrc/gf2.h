@@ -20,7 +20,7 @@
 #include <stdint.h>
 
 #ifdef __HIPCC__
-#define GF2_FN __host__ __device__ inline
+#define GF2_FN __host__ __device__ __forceinline__
 #else
 #define GF2_FN static inline
 #endif

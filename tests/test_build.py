@@ -1,0 +1,66 @@
+"""Build sanity of the gfx950 kernels (CPU: hipcc cross-compiles).
+
+Guards two failure classes found on the GPU:
+  * device helpers compiled as real calls (s_swappc) instead of being
+    inlined -- a call in the plan kernel corrupted a live register across it;
+  * the prefetch ring spilling to scratch or blowing the 128-VGPR budget that
+    16 waves per CU (one 1024-thread workgroup) need.
+"""
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "pech_amd", "csrc", "crc32c_kernels.hip")
+
+
+@pytest.fixture(scope="module")
+def device_asm():
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    d = tempfile.mkdtemp()
+    out = os.path.join(d, "k.s")
+    r = subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                        "-Rpass-analysis=kernel-resource-usage", SRC, "-o", out],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return open(out).read(), r.stderr
+
+
+def kernel_body(asm, name):
+    m = re.search(r"^%s:[^\n]*\n(.*?)s_endpgm" % name, asm, flags=re.S | re.M)
+    assert m, name
+    return m.group(1)
+
+
+@pytest.mark.parametrize("kernel", ["pech_crc32c_plan", "pech_crc32c_main"])
+def test_no_calls_no_scratch(device_asm, kernel):
+    asm, _ = device_asm
+    body = kernel_body(asm, kernel)
+    assert "s_swappc" not in body and "s_setpc" not in body, "device helper not inlined"
+    assert "scratch_" not in body and "buffer_store_dword" not in body, "register spill"
+
+
+def test_main_kernel_register_budget(device_asm):
+    _, remarks = device_asm
+    m = re.search(r"Function Name: pech_crc32c_main.*?VGPRs: (\d+).*?ScratchSize \[bytes/lane\]: (\d+)", remarks,
+                  flags=re.S)
+    assert m, remarks[-1000:]
+    vgprs, scratch = int(m.group(1)), int(m.group(2))
+    assert vgprs <= 128, f"{vgprs} VGPRs: 1024-thread workgroup would not fit one CU"
+    assert scratch == 0
+
+
+def test_main_kernel_hot_loop_shape(device_asm):
+    asm, _ = device_asm
+    body = kernel_body(asm, "pech_crc32c_main")
+    # one v_perm per table lookup, lookups folded into ds_read offsets
+    assert body.count("v_perm_b32") >= 16
+    assert "ds_read_b32" in body and "offset:128" in body
+    # the prefetch ring waits are counted, not drained
+    assert re.search(r"s_waitcnt vmcnt\([1-9]\d*\)", body)
