@@ -215,12 +215,27 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 }
 
 // ---- main kernel ----------------------------------------------------------
-// One run of rows per lane-group: `ad` = address of this lane's piece in the
-// run's first row, `nl` rows to load (>= 1), `nu` rows to use (0 = idle
-// group: loads repeat another group's rows, state ignored), `zoff` != 0 =
-// the first row's piece is a virtual zero (it may lie before the buffer, so
-// row 0 is loaded from ad + zoff -- the first real piece -- and zeroed).
-// T / nmin: max / min of nu over the wave's active groups (uniform).
+// A step gives each 8-lane group of a wave one run of rows of one buffer.
+// Per lane: `ad` = address of this lane's piece in the run's first row, `nl`
+// rows to load (>= 1), `nu` rows to use (0 = idle group: its loads repeat
+// another group's rows and its state is ignored), `zoff` != 0 = the first
+// row's piece is a virtual zero (it may lie before the buffer, so row 0 is
+// loaded from ad + zoff -- the first real piece -- and zeroed), `m` = bytes
+// from the run's end to the buffer's end (final shift), `orig` = output slot.
+// Uniform: T / nmin = max / min of nu over the active groups (T == 0: no
+// step), and the wave's cursor after the step.
+struct Step {
+	uint64_t ad;
+	uint32_t mp;  // rows after the run << 4 | tail bytes   (m = 128 rows + tail)
+	uint32_t nl, nu;
+	uint32_t oz;  // orig | (zoff / 16) << 20               (zoff <= 112)
+	uint32_t T, nmin;
+	uint32_t pos, lr, rem;
+#ifdef PECH_DEBUG_BOUNDS
+	uint64_t blo, bhi; // core of the buffer this lane loads from
+#endif
+};
+
 // The address is laundered through an empty asm: row 0 of a virtual piece is
 // zeroed after its load, and without the barrier LLVM treats the load's
 // address as "don't care" in that case and folds ad + zoff back to ad -- a
@@ -244,76 +259,184 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 	}
 	return *(g_u32x4 *)a;
 }
-#define LD_PIECE(a, tag) ld_piece((a), blo, bhi, (tag))
+#define LD_PIECE(S, a, tag) ld_piece((a), (S).blo, (S).bhi, (tag))
 #elif defined(PECH_AB_NOLOAD) // diagnostic build only: no HBM reads (wrong CRCs)
-#define LD_PIECE(a, tag) ((u32x4)((uint32_t)(a)))
-#else
-#define LD_PIECE(a, tag) (*(g_u32x4 *)(a))
+#define LD_PIECE(S, a, tag) ((u32x4)((uint32_t)(a)))
+#elif defined(PECH_TEMPORAL_LOADS) // A/B: default cache policy
+#define LD_PIECE(S, a, tag) (*(g_u32x4 *)(a))
+#else // payload bytes are read once: nontemporal (measured +8-10 % HBM rate)
+#define LD_PIECE(S, a, tag) (__builtin_nontemporal_load((g_u32x4 *)(a)))
 #endif
 
-__device__ __forceinline__ void run_rows(const uint32_t *lds, uint32_t lreg, uint64_t ad, uint32_t nl, uint32_t nu,
-					 uint32_t zoff, uint32_t T, uint32_t nmin, uint32_t &s0, uint32_t &s1,
-					 uint32_t &s2, uint32_t &s3, uint64_t blo, uint64_t bhi)
+// Work out the wave's next step from its cursor (pos, lr, rem).
+__device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const uint32_t *lds, uint32_t pos,
+					  uint32_t lr, uint32_t rem, uint32_t lane, uint32_t g8, uint32_t grp)
 {
-	constexpr uint32_t U = PECH_U;
-	const uint32_t last = nl - 1u;
-	u32x4 ring[U];
-#pragma unroll
-	for (uint32_t i = 0; i < U; ++i)
-		ring[i] = LD_PIECE(row_addr(ad, min(i, last), zoff), 1);
-	if (zoff)
-		ring[0] = (u32x4)(0u);
-	s0 = s1 = s2 = s3 = 0;
-	const uint32_t nblk = (T + U - 1) / U;
-	uint32_t blk = 0;
-	// full blocks: every lane's rows valid, prefetch stays inside every run
-	for (; blk + 1 < nblk && (blk + 2) * U <= nmin; ++blk) {
-		const uint64_t base = ad + (uint64_t)(blk + 1) * U * PECH_ROW_BYTES;
-#pragma unroll
-		for (uint32_t i = 0; i < U; ++i) {
-			const u32x4 w = ring[i];
-			ring[i] = LD_PIECE(base + i * PECH_ROW_BYTES, 2);
-			s0 = adv128(lds, s0, lreg) ^ w.x;
-			s1 = adv128(lds, s1, lreg) ^ w.y;
-			s2 = adv128(lds, s2, lreg) ^ w.z;
-			s3 = adv128(lds, s3, lreg) ^ w.w;
+	Step S;
+	S.T = 0;
+	S.nmin = 0;
+	S.ad = 0;
+	S.mp = 0;
+	S.nl = 1;
+	S.nu = 0;
+	S.oz = 0;
+#ifdef PECH_DEBUG_BOUNDS
+	S.blo = S.bhi = 0;
+#endif
+	while (rem) {
+		const uint32_t c = pos >> 10;
+		const uint32_t nzc = uni(lds[L_NZ / 4u + c]);
+		if ((pos & 1023u) >= nzc) {
+			pos = (c + 1u) << 10;
+			continue;
 		}
-	}
-	// ragged blocks: clamped prefetch, predicated update
-	for (; blk + 1 < nblk; ++blk) {
-		const uint32_t r = blk * U;
+		const pech_core cd = cores[pos];
+		const uint32_t rows0 = uni(cd.rows);
+		const uint64_t vb0 = uni64(cd.vbase);
+		const uint32_t meta0 = uni(cd.meta);
+		const uint32_t vp0 = PECH_META_VP(meta0);
+		const uint32_t avail0 = rows0 - lr;
+		if (avail0 >= PECH_SPLIT_ROWS && rem >= 64u) {
+			// one large buffer (portion): 8 contiguous slices, one per group
+			const uint32_t P = min(avail0, rem);
+			const uint32_t q = P >> 3, rm = P & 7u;
+			const uint32_t st = lr + grp * q + min(grp, rm);
+			const uint32_t nn = q + (grp < rm ? 1u : 0u);
+			S.ad = vb0 + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
+			S.nl = nn;
+			S.nu = nn;
+			S.oz = PECH_META_ORIG(meta0) | ((st == 0 && g8 < vp0) ? (vp0 - g8) << 20 : 0u);
+			S.mp = ((rows0 - st - nn) << 4) | PECH_META_TAIL(meta0);
+			S.T = q + (rm ? 1u : 0u);
+			S.nmin = q;
+#ifdef PECH_DEBUG_BOUNDS
+			S.blo = vb0 + 16u * vp0;
+			S.bhi = vb0 + (uint64_t)rows0 * PECH_ROW_BYTES;
+#endif
+			rem -= P;
+			if (P == avail0) {
+				++pos;
+				lr = 0;
+			} else {
+				lr += P;
+			}
+		} else {
+			// up to 8 neighbouring buffers, one per group.  Their descriptors
+			// come in by SCALAR loads (lgkmcnt), so waiting for them never
+			// drains the vector-load prefetch queue (vmcnt is in order).
+			// pos+7 may run past the chunk (or the cores array into lrs, still
+			// workspace memory); such entries are never used.
+			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
 #pragma unroll
-		for (uint32_t i = 0; i < U; ++i) {
-			const u32x4 w = ring[i];
-			ring[i] = LD_PIECE(row_addr(ad, min(r + U + i, last), zoff), 3);
-			const bool ok = r + i < nu;
-			const uint32_t t0 = adv128(lds, s0, lreg) ^ w.x;
-			const uint32_t t1 = adv128(lds, s1, lreg) ^ w.y;
-			const uint32_t t2 = adv128(lds, s2, lreg) ^ w.z;
-			const uint32_t t3 = adv128(lds, s3, lreg) ^ w.w;
-			s0 = ok ? t0 : s0;
-			s1 = ok ? t1 : s1;
-			s2 = ok ? t2 : s2;
-			s3 = ok ? t3 : s3;
-		}
-	}
-	// last block: no more loads
-	{
-		const uint32_t r = blk * U;
+			for (uint32_t j = 0; j < 8; ++j) {
+				const pech_core dj = cores[pos + j];
+				const bool mine = grp == j;
+				vlo = mine ? uni((uint32_t)dj.vbase) : vlo;
+				vhi = mine ? uni((uint32_t)(dj.vbase >> 32)) : vhi;
+				mrows = mine ? uni(dj.rows) : mrows;
+				mmeta = mine ? uni(dj.meta) : mmeta;
+			}
+			pech_core my;
+			my.vbase = ((uint64_t)vhi << 32) | vlo;
+			my.rows = mrows;
+			my.meta = mmeta;
+			const uint32_t myp = pos + grp;
+			const bool inchunk = (myp & 1023u) < nzc && (myp >> 10) == c;
+			const uint32_t myrows = inchunk ? my.rows : 0u;
+			// cut at the first non-first group whose buffer is split or out of chunk
+			const bool cut = grp > 0 && (!inchunk || myrows >= PECH_SPLIT_ROWS);
+			const uint64_t cutm = __ballot(cut && g8 == 0);
+			const uint32_t kcut = cutm ? (uint32_t)(__builtin_ctzll(cutm) >> 3) : 8u;
+			const uint32_t mylr = grp ? 0u : lr;
+			const uint32_t avail = grp < kcut ? myrows - mylr : 0u;
+			// exclusive prefix of avail over groups (lanes 8j)
+			uint32_t pre = avail, x;
+			x = __shfl_up(pre, 8);
+			if (lane >= 8)
+				pre += x;
+			x = __shfl_up(pre, 16);
+			if (lane >= 16)
+				pre += x;
+			x = __shfl_up(pre, 32);
+			if (lane >= 32)
+				pre += x;
+			pre -= avail;
+			const uint32_t nu = pre >= rem ? 0u : min(avail, rem - pre);
+			uint32_t tmax = nu, tmin = nu ? nu : 0xFFFFFFFFu;
 #pragma unroll
-		for (uint32_t i = 0; i < U; ++i) {
-			const u32x4 w = ring[i];
-			const bool ok = r + i < nu;
-			const uint32_t t0 = adv128(lds, s0, lreg) ^ w.x;
-			const uint32_t t1 = adv128(lds, s1, lreg) ^ w.y;
-			const uint32_t t2 = adv128(lds, s2, lreg) ^ w.z;
-			const uint32_t t3 = adv128(lds, s3, lreg) ^ w.w;
-			s0 = ok ? t0 : s0;
-			s1 = ok ? t1 : s1;
-			s2 = ok ? t2 : s2;
-			s3 = ok ? t3 : s3;
+			for (uint32_t d = 8; d < 64; d <<= 1) {
+				tmax = max(tmax, (uint32_t)__shfl_xor(tmax, d));
+				tmin = min(tmin, (uint32_t)__shfl_xor(tmin, d));
+			}
+			S.T = uni(tmax);
+			S.nmin = uni(tmin);
+			const uint32_t used = uni(min((uint32_t)__shfl(pre + avail, 63), rem));
+			const uint32_t myvp = PECH_META_VP(my.meta);
+			uint32_t zp;
+			if (nu) {
+				S.ad = my.vbase + (uint64_t)mylr * PECH_ROW_BYTES + 16u * g8;
+				S.nl = nu;
+				zp = (mylr == 0 && g8 < myvp) ? myvp - g8 : 0u;
+			} else {
+				// idle groups reload group 0's rows (valid memory), state ignored
+				S.ad = vb0 + (uint64_t)lr * PECH_ROW_BYTES + 16u * g8;
+				S.nl = min(avail0, rem);
+				zp = (lr == 0 && g8 < vp0) ? vp0 - g8 : 0u;
+			}
+			S.nu = nu;
+			S.oz = PECH_META_ORIG(my.meta) | (zp << 20);
+			S.mp = ((myrows - mylr - nu) << 4) | PECH_META_TAIL(my.meta);
+#ifdef PECH_DEBUG_BOUNDS
+			const uint64_t bv = nu ? my.vbase : vb0;
+			S.blo = bv + 16u * (nu ? myvp : vp0);
+			S.bhi = bv + (uint64_t)(nu ? myrows : rows0) * PECH_ROW_BYTES;
+#endif
+			rem -= used;
+			if (rem) { // then every group < kcut finished its buffer
+				pos += kcut;
+				lr = 0;
+			}
 		}
+		break;
 	}
+	S.pos = pos;
+	S.lr = lr;
+	S.rem = rem;
+	return S;
+}
+
+#define STEP_ZOFF(S) (((S).oz >> 16) & 0x70u) // (zoff/16) << 20 -> zoff
+#define STEP_ORIG(S) ((S).oz & 0xFFFFFu)
+#define STEP_M(S) ((uint64_t)((S).mp >> 4) * PECH_ROW_BYTES + ((S).mp & 15u))
+
+// first PECH_U rows of a step into the ring (clamped to its rows)
+#define RING_PRIME(S, ring)                                                                           \
+	do {                                                                                          \
+		const uint32_t last_ = (S).nl - 1u;                                                   \
+		_Pragma("unroll") for (uint32_t i = 0; i < PECH_U; ++i) (ring)[i] =                   \
+			LD_PIECE((S), row_addr((S).ad, min(i, last_), STEP_ZOFF(S)), 1);                 \
+	} while (0)
+
+__device__ __forceinline__ void horner_row(const uint32_t *lds, uint32_t lreg, u32x4 w, uint32_t &s0, uint32_t &s1,
+					   uint32_t &s2, uint32_t &s3)
+{
+	s0 = adv128(lds, s0, lreg) ^ w.x;
+	s1 = adv128(lds, s1, lreg) ^ w.y;
+	s2 = adv128(lds, s2, lreg) ^ w.z;
+	s3 = adv128(lds, s3, lreg) ^ w.w;
+}
+
+__device__ __forceinline__ void horner_row_pred(const uint32_t *lds, uint32_t lreg, u32x4 w, bool ok, uint32_t &s0,
+						uint32_t &s1, uint32_t &s2, uint32_t &s3)
+{
+	const uint32_t t0 = adv128(lds, s0, lreg) ^ w.x;
+	const uint32_t t1 = adv128(lds, s1, lreg) ^ w.y;
+	const uint32_t t2 = adv128(lds, s2, lreg) ^ w.z;
+	const uint32_t t3 = adv128(lds, s3, lreg) ^ w.w;
+	s0 = ok ? t0 : s0;
+	s1 = ok ? t1 : s1;
+	s2 = ok ? t2 : s2;
+	s3 = ok ? t3 : s3;
 }
 
 // Fold a group's 32 stream registers into the CRC of its run (as a message
@@ -351,6 +474,7 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts,
 	uint32_t *__restrict__ out, uint32_t rpw_min)
 {
+	constexpr uint32_t U = PECH_U;
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	const uint32_t tid = threadIdx.x;
 
@@ -359,15 +483,52 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	{
 		const uint32_t pv = tid < nchunks ? partials[tid] : 0u;
 		lds[L_NZ / 4u + tid] = tid < nchunks ? nzs[tid] : 0u;
-		const uint32_t ex = block_excl_scan(pv, lds + L_MISC / 4u, &Rtot);
+		const uint32_t ex = block_excl_scan(pv, lds + L_MISC / 4u, &Rtot); // (barriers inside)
 		lds[L_CHUNK / 4u + tid] = ex;
 	}
+	__syncthreads();
 	Rtot = uni(Rtot);
 	const uint64_t W = (uint64_t)gridDim.x * PECH_WAVES_PER_WG;
 	const uint64_t rpw64 = ((uint64_t)Rtot + W - 1) / W;
 	const uint32_t rpw = (uint32_t)(rpw64 < rpw_min ? rpw_min : rpw64);
 	if ((uint64_t)blockIdx.x * PECH_WAVES_PER_WG * rpw >= Rtot)
 		return; // whole workgroup idle (small batch)
+
+	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
+	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
+	const uint32_t wid = blockIdx.x * PECH_WAVES_PER_WG + uni(tid >> 6);
+	const uint64_t r0 = (uint64_t)wid * rpw;
+	uint32_t rem = r0 < Rtot ? uni((uint32_t)min((uint64_t)rpw, (uint64_t)Rtot - r0)) : 0u;
+
+	// First step of the wave and its first loads BEFORE staging the tables,
+	// so the prologue overlaps HBM latency.
+	u32x4 ring[U];
+	Step S;
+	S.T = 0;
+	if (rem) {
+		// locate the first buffer: chunk by binary search of the LDS prefix,
+		// then a 64-ary search of the chunk's row offsets
+		uint32_t clo = 0, chi = nchunks;
+		while (chi - clo > 1) {
+			const uint32_t mid = (clo + chi) >> 1;
+			if (uni(lds[L_CHUNK / 4u + mid]) <= r0)
+				clo = mid;
+			else
+				chi = mid;
+		}
+		const uint32_t rr = uni((uint32_t)(r0 - lds[L_CHUNK / 4u + clo]));
+		uint32_t plo = clo * PECH_CHUNK, phi = plo + uni(lds[L_NZ / 4u + clo]);
+		while (phi - plo > 1) {
+			const uint32_t step = (phi - plo + 63u) >> 6;
+			const uint32_t p = plo + lane * step;
+			const bool ok = p < phi && lrs[p] <= rr;
+			const uint32_t cnt = (uint32_t)__popcll(__ballot(ok));
+			plo = uni(plo + (cnt - 1u) * step);
+			phi = uni(min(phi, plo + step));
+		}
+		S = plan_step(cores, lds, plo, uni(rr - lrs[plo]), rem, lane, g8, grp);
+		RING_PRIME(S, ring);
+	}
 
 	// stage the tables: A_128 once per bank, the rest single copy
 	for (uint32_t j = tid; j < 8192u; j += PECH_WG_THREADS) {
@@ -383,142 +544,51 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	}
 	__syncthreads();
 
-	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
-	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
-	const uint32_t wid = blockIdx.x * PECH_WAVES_PER_WG + uni(tid >> 6);
-	const uint64_t r0 = (uint64_t)wid * rpw;
-	if (r0 >= Rtot)
-		return;
-	uint32_t rem = uni((uint32_t)min((uint64_t)rpw, (uint64_t)Rtot - r0));
-
-	// locate the first buffer: chunk by binary search of the LDS prefix, then
-	// a 64-ary search of the chunk's row offsets (2 rounds for 1024 entries)
-	uint32_t clo = 0, chi = nchunks;
-	while (chi - clo > 1) {
-		const uint32_t mid = (clo + chi) >> 1;
-		if (uni(lds[L_CHUNK / 4u + mid]) <= r0)
-			clo = mid;
-		else
-			chi = mid;
-	}
-	const uint32_t rr = uni((uint32_t)(r0 - lds[L_CHUNK / 4u + clo]));
-	uint32_t plo = clo * PECH_CHUNK, phi = plo + uni(lds[L_NZ / 4u + clo]);
-	while (phi - plo > 1) {
-		const uint32_t step = (phi - plo + 63u) >> 6;
-		const uint32_t p = plo + lane * step;
-		const bool ok = p < phi && lrs[p] <= rr;
-		const uint64_t bal = __ballot(ok);
-		const uint32_t cnt = (uint32_t)__popcll(bal);
-#ifdef PECH_DEBUG_BOUNDS
-		if (blockIdx.x == 0 && wid == 3 && p < phi && (lane < 3 || (lane + 3 >= cnt && lane <= cnt + 1)))
-			printf("PECH TRACE search plo %u phi %u step %u lane %u p %u lrs %u ok %d bal %llx cnt %u\n", plo, phi,
-			       step, lane, p, lrs[p], (int)ok, (unsigned long long)bal, cnt);
-#endif
-		plo = uni(plo + (cnt - 1u) * step);
-		phi = uni(min(phi, plo + step));
-	}
-	uint32_t pos = plo;
-	uint32_t lr = uni(rr - lrs[pos]);
-#ifdef PECH_DEBUG_BOUNDS
-	const bool trace = blockIdx.x == 0 && wid == 3 && lane == 0;
-	if (trace)
-		printf("PECH TRACE wid %u r0 %llu rem %u Rtot %u rpw %u clo %u rr %u pos %u lrs[pos] %u lr %u nz %u\n", wid,
-		       (unsigned long long)r0, rem, Rtot, rpw, clo, rr, pos, lrs[pos], lr, lds[L_NZ / 4u + clo]);
-#endif
-
-	while (rem) {
-		const uint32_t c = pos >> 10;
-		if ((pos & 1023u) >= uni(lds[L_NZ / 4u + c])) {
-			pos = (c + 1u) << 10;
-			continue;
+	while (S.T) {
+		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+		if (STEP_ZOFF(S))
+			ring[0] = (u32x4)(0u);
+		const uint32_t nblk = (S.T + U - 1) / U;
+		const uint32_t last = S.nl - 1u;
+		uint32_t blk = 0;
+		// full blocks: every lane's rows valid, prefetch stays inside every run
+		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
+			const uint64_t base = S.ad + (uint64_t)(blk + 1) * U * PECH_ROW_BYTES;
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i) {
+				const u32x4 w = ring[i];
+				ring[i] = LD_PIECE(S, base + i * PECH_ROW_BYTES, 2);
+				horner_row(lds, lreg, w, s0, s1, s2, s3);
+			}
 		}
-		const pech_core cd = cores[pos];
-		const uint32_t rows0 = uni(cd.rows);
-		const uint32_t avail0 = rows0 - lr;
-#ifdef PECH_DEBUG_BOUNDS
-		if (trace)
-			printf("PECH TRACE step pos %u lr %u rem %u rows0 %u\n", pos, lr, rem, rows0);
-#endif
-		uint32_t s0, s1, s2, s3;
-		if (avail0 >= PECH_SPLIT_ROWS && rem >= 64u) {
-			// one large buffer (portion): 8 contiguous slices, one per group
-			const uint32_t P = min(avail0, rem);
-			const uint32_t q = P >> 3, rm = P & 7u;
-			const uint32_t st = lr + grp * q + min(grp, rm);
-			const uint32_t nn = q + (grp < rm ? 1u : 0u);
-			const uint64_t ad = uni64(cd.vbase) + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
-			const uint32_t meta = uni(cd.meta);
-			const uint32_t vp = PECH_META_VP(meta);
-			const uint32_t zoff = (st == 0 && g8 < vp) ? 16u * (vp - g8) : 0u;
-			const uint64_t vb = uni64(cd.vbase);
-			run_rows(lds, lreg, ad, nn, nn, zoff, q + (rm ? 1u : 0u), q, s0, s1, s2, s3, vb + 16u * vp,
-				 vb + (uint64_t)rows0 * PECH_ROW_BYTES);
-			const uint64_t m = (uint64_t)(rows0 - st - nn) * PECH_ROW_BYTES + PECH_META_TAIL(meta);
-			finish_run(lds, g8, s0, s1, s2, s3, m, true, out, PECH_META_ORIG(meta));
-			rem -= P;
-			if (P == avail0) {
-				++pos;
-				lr = 0;
-			} else {
-				lr += P;
+		// ragged blocks: clamped prefetch, predicated update
+		for (; blk + 1 < nblk; ++blk) {
+			const uint32_t r = blk * U;
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i) {
+				const u32x4 w = ring[i];
+				ring[i] = LD_PIECE(S, row_addr(S.ad, min(r + U + i, last), STEP_ZOFF(S)), 3);
+				horner_row_pred(lds, lreg, w, r + i < S.nu, s0, s1, s2, s3);
+			}
+		}
+		// last block: its loads already fetch the next step's first rows
+		const Step N = plan_step(cores, lds, S.pos, S.lr, S.rem, lane, g8, grp);
+		const uint32_t r = blk * U;
+		if (N.T) {
+			const uint32_t nlast = N.nl - 1u;
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i) {
+				const u32x4 w = ring[i];
+				ring[i] = LD_PIECE(N, row_addr(N.ad, min(i, nlast), STEP_ZOFF(N)), 4);
+				horner_row_pred(lds, lreg, w, r + i < S.nu, s0, s1, s2, s3);
 			}
 		} else {
-			// up to 8 neighbouring buffers, one per group
-			const uint32_t nzc = uni(lds[L_NZ / 4u + c]);
-			const uint32_t myp = pos + grp;
-			const bool inchunk = (myp & 1023u) < nzc && (myp >> 10) == c;
-			pech_core my = cd;
-			if (grp && inchunk)
-				my = cores[myp];
-			const uint32_t myrows = inchunk ? my.rows : 0u;
-			// cut at the first non-first group whose buffer is large or out of chunk
-			const bool cut = grp > 0 && (!inchunk || myrows >= PECH_SPLIT_ROWS);
-			const uint64_t cutm = __ballot(cut && g8 == 0);
-			const uint32_t kcut = cutm ? (uint32_t)(__builtin_ctzll(cutm) >> 3) : 8u;
-			const uint32_t mylr = grp ? 0u : lr;
-			const uint32_t avail = grp < kcut ? myrows - mylr : 0u;
-			// exclusive prefix of avail over groups (lanes 8j)
-			uint32_t pre = avail, x;
-			x = __shfl_up(pre, 8);
-			if (lane >= 8)
-				pre += x;
-			x = __shfl_up(pre, 16);
-			if (lane >= 16)
-				pre += x;
-			x = __shfl_up(pre, 32);
-			if (lane >= 32)
-				pre += x;
-			pre -= avail;
-			const uint32_t nu = pre >= rem ? 0u : min(avail, rem - pre);
-			// uniform T = max nu, nmin = min nu over active groups
-			uint32_t tmax = nu, tmin = nu ? nu : 0xFFFFFFFFu;
 #pragma unroll
-			for (uint32_t d = 8; d < 64; d <<= 1) {
-				tmax = max(tmax, (uint32_t)__shfl_xor(tmax, d));
-				tmin = min(tmin, (uint32_t)__shfl_xor(tmin, d));
-			}
-			const uint32_t T = uni(tmax), nmin = uni(tmin);
-			const uint32_t used = uni(min((uint32_t)__shfl(pre + avail, 63), rem));
-			// idle groups reload group 0's rows (valid memory), state ignored
-			const uint64_t ad0 = uni64(cd.vbase) + (uint64_t)lr * PECH_ROW_BYTES + 16u * g8;
-			const uint32_t vp0 = PECH_META_VP(uni(cd.meta));
-			const uint32_t z0 = (lr == 0 && g8 < vp0) ? 16u * (vp0 - g8) : 0u;
-			const uint32_t n0 = min(avail0, rem);
-			const uint32_t myvp = PECH_META_VP(my.meta);
-			const uint32_t zm = (mylr == 0 && g8 < myvp) ? 16u * (myvp - g8) : 0u;
-			const uint64_t ad = nu ? my.vbase + (uint64_t)mylr * PECH_ROW_BYTES + 16u * g8 : ad0;
-			const uint64_t bv = nu ? my.vbase : uni64(cd.vbase);
-			const uint32_t bvp = nu ? myvp : vp0, brows = nu ? myrows : rows0;
-			run_rows(lds, lreg, ad, nu ? nu : n0, nu, nu ? zm : z0, T, nmin, s0, s1, s2, s3, bv + 16u * bvp,
-				 bv + (uint64_t)brows * PECH_ROW_BYTES);
-			const uint64_t m = (uint64_t)(myrows - mylr - nu) * PECH_ROW_BYTES + PECH_META_TAIL(my.meta);
-			finish_run(lds, g8, s0, s1, s2, s3, m, nu != 0, out, PECH_META_ORIG(my.meta));
-			rem -= used;
-			if (rem) { // then every group < kcut finished its buffer
-				pos += kcut;
-				lr = 0;
-			}
+			for (uint32_t i = 0; i < U; ++i)
+				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
 		}
+		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));
+		S = N;
 	}
 }
 
