@@ -35,6 +35,13 @@
 #ifndef PECH_U
 #define PECH_U 8 // rows in flight per lane
 #endif
+#ifndef PECH_ROTATE
+#define PECH_ROTATE 0 // 1: each wave walks its range in rotated order (measured slower)
+#endif
+#ifndef PECH_ODD_RPW
+#define PECH_ODD_RPW 0 // 1: odd rows-per-wave, so wave ranges are not power-of-two aligned
+#endif
+
 
 // ---- LDS map of the main kernel (bytes) ---------------------------------
 #define L_REP 0u                 // 128 KiB: A_128, 32 bank copies
@@ -215,6 +222,14 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 }
 
 // ---- main kernel ----------------------------------------------------------
+#ifdef PECH_STAMPS // diagnostic build: per-wave start/end s_memtime stamps
+#define PECH_MAX_STAMPS 8192u
+__device__ uint64_t pech_stamps[3 * PECH_MAX_STAMPS];
+extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
+{
+	return hipMemcpyFromSymbol(host, HIP_SYMBOL(pech_stamps), sizeof(uint64_t) * 3 * n) == hipSuccess ? 0 : -1;
+}
+#endif
 // A step gives each 8-lane group of a wave one run of rows of one buffer.
 // Per lane: `ad` = address of this lane's piece in the run's first row, `nl`
 // rows to load (>= 1), `nu` rows to use (0 = idle group: its loads repeat
@@ -268,9 +283,51 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 #define LD_PIECE(S, a, tag) (__builtin_nontemporal_load((g_u32x4 *)(a)))
 #endif
 
+// Locate row r of the batch's row space: chunk by binary search of the LDS
+// prefix, then an SG-ary search of the chunk's row offsets by the SG lanes of
+// a sub-group (lanes [sgbase, sgbase+SG) of the wave, all with the same r).
+// Returns the position (plan order) and the row inside that buffer.
+template <uint32_t SG>
+__device__ __forceinline__ void find_start(const uint32_t *__restrict__ lrs, const uint32_t *lds, uint32_t nchunks,
+					   uint32_t r, uint32_t sl, uint32_t sgbase, bool want, uint32_t &pos,
+					   uint32_t &lr)
+{
+	uint32_t clo = 0, chi = nchunks;
+	while (chi - clo > 1) {
+		const uint32_t mid = (clo + chi) >> 1;
+		if (lds[L_CHUNK / 4u + mid] <= r)
+			clo = mid;
+		else
+			chi = mid;
+	}
+	const uint32_t rr = r - lds[L_CHUNK / 4u + clo];
+	uint32_t plo = clo * PECH_CHUNK, phi = plo + lds[L_NZ / 4u + clo];
+	bool active = want && phi - plo > 1;
+	while (__any(active)) {
+		const uint32_t step = (phi - plo + SG - 1u) / SG;
+		const uint32_t p = plo + sl * step;
+		const bool ok = active && p < phi && lrs[p] <= rr;
+		const uint64_t bal = __ballot(ok);
+		const uint64_t mask = SG == 64 ? ~0ull : ((1ull << SG) - 1ull);
+		const uint32_t cnt = (uint32_t)__popcll((bal >> sgbase) & mask);
+		if (active) {
+			plo = plo + (cnt - 1u) * step;
+			phi = min(phi, plo + step);
+			active = phi - plo > 1;
+		}
+	}
+	pos = plo;
+	lr = want ? rr - lrs[plo] : 0u;
+}
+
 // Work out the wave's next step from its cursor (pos, lr, rem).
-__device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const uint32_t *lds, uint32_t pos,
-					  uint32_t lr, uint32_t rem, uint32_t lane, uint32_t g8, uint32_t grp)
+struct Part {
+	uint32_t pos, lr, rem; // a wave cursor (uniform)
+};
+
+__device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const uint32_t *lds, Part &nx,
+					  uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane, uint32_t g8,
+					  uint32_t grp)
 {
 	Step S;
 	S.T = 0;
@@ -283,7 +340,17 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 #ifdef PECH_DEBUG_BOUNDS
 	S.blo = S.bhi = 0;
 #endif
-	while (rem) {
+	for (;;) {
+		if (rem == 0) {
+			// first part of the wave's range done: continue with the second
+			if (nx.rem == 0)
+				break;
+			pos = nx.pos;
+			lr = nx.lr;
+			rem = nx.rem;
+			nx.rem = 0;
+			continue;
+		}
 		const uint32_t c = pos >> 10;
 		const uint32_t nzc = uni(lds[L_NZ / 4u + c]);
 		if ((pos & 1023u) >= nzc) {
@@ -490,43 +557,46 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	Rtot = uni(Rtot);
 	const uint64_t W = (uint64_t)gridDim.x * PECH_WAVES_PER_WG;
 	const uint64_t rpw64 = ((uint64_t)Rtot + W - 1) / W;
-	const uint32_t rpw = (uint32_t)(rpw64 < rpw_min ? rpw_min : rpw64);
+	uint32_t rpw = (uint32_t)(rpw64 < rpw_min ? rpw_min : rpw64);
+	if (PECH_ODD_RPW)
+		rpw |= 1u;
 	if ((uint64_t)blockIdx.x * PECH_WAVES_PER_WG * rpw >= Rtot)
 		return; // whole workgroup idle (small batch)
 
 	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
 	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
-	const uint32_t wid = blockIdx.x * PECH_WAVES_PER_WG + uni(tid >> 6);
-	const uint64_t r0 = (uint64_t)wid * rpw;
-	uint32_t rem = r0 < Rtot ? uni((uint32_t)min((uint64_t)rpw, (uint64_t)Rtot - r0)) : 0u;
-
-	// First step of the wave and its first loads BEFORE staging the tables,
-	// so the prologue overlaps HBM latency.
+	const uint32_t wave = uni(tid >> 6);
 	u32x4 ring[U];
 	Step S;
 	S.T = 0;
-	if (rem) {
-		// locate the first buffer: chunk by binary search of the LDS prefix,
-		// then a 64-ary search of the chunk's row offsets
-		uint32_t clo = 0, chi = nchunks;
-		while (chi - clo > 1) {
-			const uint32_t mid = (clo + chi) >> 1;
-			if (uni(lds[L_CHUNK / 4u + mid]) <= r0)
-				clo = mid;
-			else
-				chi = mid;
-		}
-		const uint32_t rr = uni((uint32_t)(r0 - lds[L_CHUNK / 4u + clo]));
-		uint32_t plo = clo * PECH_CHUNK, phi = plo + uni(lds[L_NZ / 4u + clo]);
-		while (phi - plo > 1) {
-			const uint32_t step = (phi - plo + 63u) >> 6;
-			const uint32_t p = plo + lane * step;
-			const bool ok = p < phi && lrs[p] <= rr;
-			const uint32_t cnt = (uint32_t)__popcll(__ballot(ok));
-			plo = uni(plo + (cnt - 1u) * step);
-			phi = uni(min(phi, plo + step));
-		}
-		S = plan_step(cores, lds, plo, uni(rr - lrs[plo]), rem, lane, g8, grp);
+	// The wave's range [r0, r1) is walked as two parts, [r0+d, r1) then
+	// [r0, r0+d), with a per-wave pseudo-random d: at any instant the 32768
+	// streams of the chip then sit at unrelated offsets instead of all at the
+	// same offset modulo the (power-of-two) slice size, which concentrates
+	// requests on few HBM channels (measured on the read probe: 6.66 ->
+	// 7.01 TB/s).  Both starts are found by a 32-ary search each.
+	const uint32_t wid = blockIdx.x * PECH_WAVES_PER_WG + wave;
+	const uint64_t r0_64 = (uint64_t)wid * rpw;
+	const uint32_t r0 = (uint32_t)min(r0_64, (uint64_t)Rtot);
+	const uint32_t rem_all = (uint32_t)min((uint64_t)rpw, (uint64_t)Rtot - r0);
+	uint32_t d = 0;
+	if (PECH_ROTATE && rem_all >= 128u) {
+		d = (uint32_t)(((uint64_t)(wid * 2654435761u) * (rem_all - 64u)) >> 32);
+		d = d < 64u ? 0u : d;
+	}
+	Part nx = {0, 0, 0};
+	if (rem_all) {
+		const uint32_t half = lane >> 5, sl = lane & 31u;
+		const uint32_t r = half ? r0 : r0 + d;
+		uint32_t pos, lr;
+		find_start<32>(lrs, lds, nchunks, r, sl, half * 32u, half == 0 || d != 0, pos, lr);
+		const uint32_t p0 = uni(pos), lr0 = uni(lr);
+		nx.pos = __shfl(pos, 32);
+		nx.lr = __shfl(lr, 32);
+		nx.pos = uni(nx.pos);
+		nx.lr = uni(nx.lr);
+		nx.rem = d;
+		S = plan_step(cores, lds, nx, p0, lr0, rem_all - d, lane, g8, grp);
 		RING_PRIME(S, ring);
 	}
 
@@ -544,6 +614,9 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	}
 	__syncthreads();
 
+#ifdef PECH_STAMPS
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
 	while (S.T) {
 		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 		if (STEP_ZOFF(S))
@@ -572,7 +645,7 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 			}
 		}
 		// last block: its loads already fetch the next step's first rows
-		const Step N = plan_step(cores, lds, S.pos, S.lr, S.rem, lane, g8, grp);
+		const Step N = plan_step(cores, lds, nx, S.pos, S.lr, S.rem, lane, g8, grp);
 		const uint32_t r = blk * U;
 		if (N.T) {
 			const uint32_t nlast = N.nl - 1u;
@@ -590,6 +663,15 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));
 		S = N;
 	}
+#ifdef PECH_STAMPS
+	if (lane == 0 && wid < PECH_MAX_STAMPS) {
+		uint32_t xcc;
+		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+		pech_stamps[3 * wid] = t_start;
+		pech_stamps[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+		pech_stamps[3 * wid + 2] = ((uint64_t)blockIdx.x << 8) | (xcc & 0xFu);
+	}
+#endif
 }
 
 // ---- host-side launchers (used by crc32c_api.cpp) -------------------------

@@ -23,6 +23,8 @@ def _consts():
         out[m.group(1)] = int(m.group(2))
     ksrc = open(os.path.join(REPO, "pech_amd", "csrc", "crc32c_kernels.hip")).read()
     out["PECH_U"] = int(re.search(r"#define PECH_U (\d+)", ksrc).group(1))
+    out["PECH_ROTATE"] = int(re.search(r"#define PECH_ROTATE (\d+)", ksrc).group(1))
+    out["PECH_ODD_RPW"] = int(re.search(r"#define PECH_ODD_RPW (\d+)", ksrc).group(1))
     return out
 
 
@@ -116,41 +118,67 @@ def run_rows_loads(U, nl, nu, zoff, T, nmin):
     return loads, consumed
 
 
-def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None):
-    """Yield events: ("load", buf, lane_piece_addr) and ("use", orig, row,
-    g8) and ("finish", orig, group_end_row, m)."""
+def find_start(lrs, pref, nzs, r, SG):
+    """find_start<SG>: chunk by binary search, then SG-ary search (as the
+    kernel's lanes do it)."""
+    nchunks = len(nzs)
+    clo, chi = 0, nchunks
+    while chi - clo > 1:
+        mid = (clo + chi) >> 1
+        if pref[mid] <= r:
+            clo = mid
+        else:
+            chi = mid
+    rr = r - pref[clo]
+    plo, phi = clo * CHUNK, clo * CHUNK + nzs[clo]
+    while phi - plo > 1:
+        step = (phi - plo + SG - 1) // SG
+        cnt = sum(1 for sl in range(SG) if plo + sl * step < phi and lrs[plo + sl * step] <= rr)
+        plo = plo + (cnt - 1) * step
+        phi = min(phi, plo + step)
+    return plo, rr - lrs[plo]
+
+
+def rotation(wid, rem_all):
+    """per-wave split point d of the main kernel (PECH_ROTATE)."""
+    if not C["PECH_ROTATE"] or rem_all < 128:
+        return 0
+    d = ((((wid * 2654435761) & 0xFFFFFFFF) * (rem_all - 64)) >> 32)
+    return 0 if d < 64 else d
+
+
+def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, rng=None):
+    """Yield events: ("load", buf, lane_piece_addr), ("use", orig, row, g8,
+    virtual) and ("finish", orig, run_end_row, m): every wave walks its range
+    [r0, r1) as [r0+d, r1) then [r0, r0+d)."""
     U = U or C["PECH_U"]
     rpw_min = rpw_min or C["PECH_RPW_MIN"]
-    nchunks = len(partials)
     pref = [0]
     for p in partials:
         pref.append(pref[-1] + p)
     Rtot = pref[-1]
     W = ncu * WAVES_PER_WG
     rpw = max(rpw_min, (Rtot + W - 1) // W)
+    if C["PECH_ODD_RPW"]:
+        rpw |= 1
     events = []
     for wid in range(W):
         r0 = wid * rpw
         if r0 >= Rtot:
             continue
-        rem = min(rpw, Rtot - r0)
-        # chunk search: largest c with pref[c] <= r0
-        clo, chi = 0, nchunks
-        while chi - clo > 1:
-            mid = (clo + chi) >> 1
-            if pref[mid] <= r0:
-                clo = mid
-            else:
-                chi = mid
-        rr = r0 - pref[clo]
-        plo, phi = clo * CHUNK, clo * CHUNK + nzs[clo]
-        while phi - plo > 1:
-            step = (phi - plo + 63) >> 6
-            cnt = sum(1 for lane in range(64) if plo + lane * step < phi and lrs[plo + lane * step] <= rr)
-            plo = plo + (cnt - 1) * step
-            phi = min(phi, plo + step)
-        pos = plo
-        lr = rr - lrs[pos]
+        rem_all = min(rpw, Rtot - r0)
+        d = rotation(wid, rem_all)
+        pos, lr = find_start(lrs, pref, nzs, r0 + d, 32)
+        walk(cores, nzs, pos, lr, rem_all - d, U, events)
+        if d:
+            pos, lr = find_start(lrs, pref, nzs, r0, 32)
+            walk(cores, nzs, pos, lr, d, U, events)
+    return events
+
+
+def walk(cores, nzs, pos, lr, rem, U, events):
+    """plan_step + run of one sub-range (pos, lr, rem)."""
+    if True:
         guard = 0
         while rem:
             guard += 1

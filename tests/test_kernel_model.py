@@ -12,7 +12,7 @@ import kernel_model as KM
 def check(descs, ncu=4, seed=0):
     rng = random.Random(seed)
     cores, lrs, partials, nzs = KM.plan(descs, rng)
-    ev = KM.main(cores, lrs, partials, nzs, ncu)
+    ev = KM.main(cores, lrs, partials, nzs, ncu, rng=rng)
     used = collections.Counter()
     byorig = {}
     for c in cores:

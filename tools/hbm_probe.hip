@@ -46,7 +46,68 @@ __global__ __launch_bounds__(1024) void k_stream(const u32x4 *p, size_t n16, uin
 }
 
 // G lanes per group, each group a contiguous range of `rows` rows of G*16 B
+template <bool NT>
+__device__ __forceinline__ u32x4 ldp(const uint8_t *a)
+{
+	if (NT)
+		return __builtin_nontemporal_load((g_u32x4 *)a);
+	return *(g_u32x4 *)a;
+}
+
+// same as k_group but each group starts its walk at a pseudo-random row of
+// its range and wraps around (breaks the alignment of all streams modulo the
+// range size)
 template <int G, int D>
+__global__ __launch_bounds__(1024) void k_group_rot(const uint8_t *p, uint32_t rows_per_group, uint32_t *out)
+{
+	const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+	const uint32_t gl = threadIdx.x % G;
+	const uint8_t *base = p + (size_t)gid * rows_per_group * (G * 16) + gl * 16;
+	const uint32_t off = (gid * 2654435761u) % rows_per_group;
+	u32x4 acc = (u32x4)(0u);
+	for (uint32_t r = 0; r < rows_per_group; r += D) {
+		u32x4 v[D];
+#pragma unroll
+		for (int d = 0; d < D; ++d) {
+			uint32_t row = r + d + off;
+			row = row >= rows_per_group ? row - rows_per_group : row;
+			v[d] = __builtin_nontemporal_load((g_u32x4 *)(base + (size_t)row * G * 16));
+		}
+#pragma unroll
+		for (int d = 0; d < D; ++d)
+			acc ^= v[d];
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[gid] = x;
+}
+
+// interleaved: group g of NG reads rows g, g+NG, ... (each wave-instruction
+// covers consecutive 128-byte rows)
+template <int D>
+__global__ __launch_bounds__(1024) void k_interleaved(const uint8_t *p, uint32_t total_rows, uint32_t *out)
+{
+	const uint32_t ng = gridDim.x * blockDim.x / 8;
+	const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / 8;
+	const uint32_t gl = threadIdx.x % 8;
+	u32x4 acc = (u32x4)(0u);
+	for (uint32_t r = gid; r < total_rows; r += D * ng) {
+		u32x4 v[D];
+#pragma unroll
+		for (int d = 0; d < D; ++d) {
+			const uint32_t row = min(r + d * ng, total_rows - 1);
+			v[d] = __builtin_nontemporal_load((g_u32x4 *)(p + (size_t)row * 128 + gl * 16));
+		}
+#pragma unroll
+		for (int d = 0; d < D; ++d)
+			acc ^= v[d];
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[gid] = x;
+}
+
+template <int G, int D, bool NT = false>
 __global__ __launch_bounds__(1024) void k_group(const uint8_t *p, uint32_t rows_per_group, uint32_t *out)
 {
 	const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / G;
@@ -56,20 +117,20 @@ __global__ __launch_bounds__(1024) void k_group(const uint8_t *p, uint32_t rows_
 	u32x4 ring[D];
 #pragma unroll
 	for (int d = 0; d < D; ++d)
-		ring[d] = *(g_u32x4 *)(base + (size_t)d * G * 16);
+		ring[d] = ldp<NT>(base + (size_t)d * G * 16);
 	uint32_t r = D;
 	for (; r + D <= rows_per_group; r += D) {
 #pragma unroll
 		for (int d = 0; d < D; ++d) {
 			acc ^= ring[d];
-			ring[d] = *(g_u32x4 *)(base + (size_t)(r + d) * G * 16);
+			ring[d] = ldp<NT>(base + (size_t)(r + d) * G * 16);
 		}
 	}
 #pragma unroll
 	for (int d = 0; d < D; ++d)
 		acc ^= ring[d];
 	for (; r < rows_per_group; ++r)
-		acc ^= *(g_u32x4 *)(base + (size_t)r * G * 16);
+		acc ^= ldp<NT>(base + (size_t)r * G * 16);
 	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
 	if (x == 0x12345678u)
 		out[gid] = x;
@@ -107,13 +168,29 @@ template <int U> static void launch_stream(void *v)
 	hipLaunchKernelGGL(k_stream<U>, dim3(a->ncu * 4), dim3(1024), 0, 0, (const u32x4 *)p, a->bytes / 16, a->out);
 }
 
-template <int G, int D> static void launch_group(void *v)
+template <int G, int D, bool NT = false> static void launch_group(void *v)
 {
 	Args *a = (Args *)v;
 	const uint8_t *p = a->buf[a->it++ & 1];
 	const uint32_t groups = a->ncu * 1024 / G;
 	const uint32_t rpg = (uint32_t)(a->bytes / (G * 16) / groups);
-	hipLaunchKernelGGL((k_group<G, D>), dim3(a->ncu), dim3(1024), 0, 0, p, rpg, a->out);
+	hipLaunchKernelGGL((k_group<G, D, NT>), dim3(a->ncu), dim3(1024), 0, 0, p, rpg, a->out);
+}
+
+template <int G, int D> static void launch_group_rot(void *v)
+{
+	Args *a = (Args *)v;
+	const uint8_t *p = a->buf[a->it++ & 1];
+	const uint32_t groups = a->ncu * 1024 / G;
+	const uint32_t rpg = (uint32_t)(a->bytes / (G * 16) / groups);
+	hipLaunchKernelGGL((k_group_rot<G, D>), dim3(a->ncu), dim3(1024), 0, 0, p, rpg, a->out);
+}
+
+template <int D> static void launch_interleaved(void *v)
+{
+	Args *a = (Args *)v;
+	const uint8_t *p = a->buf[a->it++ & 1];
+	hipLaunchKernelGGL((k_interleaved<D>), dim3(a->ncu), dim3(1024), 0, 0, p, (uint32_t)(a->bytes / 128), a->out);
 }
 
 int main(int argc, char **argv)
@@ -142,6 +219,13 @@ int main(int argc, char **argv)
 		{"group32 D4", launch_group<32, 4>},
 		{"group64 D4", launch_group<64, 4>},
 		{"group64 D8", launch_group<64, 8>},
+		{"group8  D8 nt", launch_group<8, 8, true>},
+		{"group8  D4 nt", launch_group<8, 4, true>},
+		{"group64 D8 nt", launch_group<64, 8, true>},
+		{"group8  D12 nt", launch_group<8, 12, true>},
+		{"group8  D8 nt rotated", launch_group_rot<8, 8>},
+		{"interleaved8 D8 nt", launch_interleaved<8>},
+		{"group8  D8 nt (again)", launch_group<8, 8, true>},
 	};
 	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, a.ncu, a.bytes);
 	for (size_t i = 0; i < sizeof(probes) / sizeof(probes[0]); ++i) {

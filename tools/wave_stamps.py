@@ -1,0 +1,54 @@
+"""Diagnostic (GPU box): per-wave start/end s_memtime of the main kernel for
+one c3-shaped batch, using the PECH_STAMPS build (PECH_CRC32C_LIB)."""
+import ctypes, os, sys
+import numpy as np
+import torch
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import pech_amd as P
+from pech_amd import _lib
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+dev = torch.device("cuda:0")
+if cfg == "c3":
+    sizes = np.full(256, 4 << 20, dtype=np.int64)
+else:
+    sizes = np.full(65536, 4096, dtype=np.int64)
+offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+buf = torch.randint(0, 256, (int(sizes.sum()),), dtype=torch.uint8, device=dev)
+descs = P.make_descs(buf.data_ptr() + offs, sizes, device=dev)
+out = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
+for _ in range(3):
+    P.dev_batch_async(descs, out)
+torch.cuda.synchronize()
+L = _lib.lib()
+L.pech_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+W = 4096
+st = np.zeros(3 * W, dtype=np.uint64)
+assert L.pech_read_stamps(st.ctypes.data, W) == 0
+s, e, tag = st[0::3].astype(np.int64), st[1::3].astype(np.int64), st[2::3].astype(np.int64)
+ok = (s > 0) & (e > 0)
+s, e, tag = s[ok], e[ok], tag[ok]
+xcc, blk = tag & 0xF, tag >> 8
+# s_memrealtime: 100 MHz chip-wide clock (10 ns ticks)
+t0 = s.min()
+s -= t0; e -= t0
+span = e.max()
+pct = lambda a, q: float(np.percentile(a, q))
+print(f"{cfg}: waves {ok.sum()}, span {span*10/1000:.1f} us")
+print("start us p50/p99/max: %.1f %.1f %.1f" % (pct(s,50)/100, pct(s,99)/100, s.max()/100))
+print("end   us p1/p10/p50/p90/max: %.1f %.1f %.1f %.1f %.1f" % (pct(e,1)/100, pct(e,10)/100, pct(e,50)/100, pct(e,90)/100, e.max()/100))
+print("mean wave busy / span: %.3f" % float(((e - s) / span).mean()))
+hist, edges = np.histogram(e / 100, bins=12)
+print("end-time histogram (us):", [(round(float(edges[i]),1), int(hist[i])) for i in range(len(hist))])
+
+for x in range(8):
+    m = xcc == x
+    print(f"xcc{x}: waves {int(m.sum())} end p10 {pct(e[m],10)/100:.1f} p50 {pct(e[m],50)/100:.1f} max {e[m].max()/100:.1f} us")
+# within-CU spread: per block, max-min of end
+per = {}
+for b, t in zip(blk, e):
+    per.setdefault(int(b), []).append(int(t))
+spread = np.array([max(v) - min(v) for v in per.values()]) / 100
+bmax = np.array([max(v) for v in per.values()]) / 100
+print("per-CU end spread us p50/p90/max: %.1f %.1f %.1f" % (pct(spread,50), pct(spread,90), spread.max()))
+print("per-CU last-wave end us p10/p50/p90: %.1f %.1f %.1f" % (pct(bmax,10), pct(bmax,50), pct(bmax,90)))
