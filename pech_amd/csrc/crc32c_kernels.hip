@@ -35,6 +35,10 @@
 #ifndef PECH_U
 #define PECH_U 8 // rows in flight per lane
 #endif
+#ifndef PECH_MAIN_WAVES
+#define PECH_MAIN_WAVES 16 // waves per main-kernel workgroup (one workgroup per CU)
+#endif
+#define PECH_MAIN_THREADS (64u * PECH_MAIN_WAVES)
 #ifndef PECH_ROTATE
 #define PECH_ROTATE 0 // 1: each wave walks its range in rotated order (measured slower)
 #endif
@@ -73,7 +77,8 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v)
 	return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
-// 1024-thread exclusive scan; scratch = 16 LDS words
+// NT-thread exclusive scan; scratch = NT/64 LDS words
+template <uint32_t NT = PECH_WG_THREADS>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t *total)
 {
 	const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -89,7 +94,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratc
 	__syncthreads();
 	uint32_t off = 0, tot = 0;
 #pragma unroll
-	for (uint32_t w = 0; w < PECH_WAVES_PER_WG; ++w) {
+	for (uint32_t w = 0; w < NT / 64u; ++w) {
 		const uint32_t t = scratch[w];
 		off += (w < wave) ? t : 0u;
 		tot += t;
@@ -536,7 +541,7 @@ __device__ __forceinline__ void finish_run(const uint32_t *lds, uint32_t g8, uin
 	}
 }
 
-extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_main(
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_main(
 	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
 	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts,
 	uint32_t *__restrict__ out, uint32_t rpw_min)
@@ -548,19 +553,31 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	// chunk row offsets, non-empty counts and the batch's total row count
 	uint32_t Rtot;
 	{
-		const uint32_t pv = tid < nchunks ? partials[tid] : 0u;
-		lds[L_NZ / 4u + tid] = tid < nchunks ? nzs[tid] : 0u;
-		const uint32_t ex = block_excl_scan(pv, lds + L_MISC / 4u, &Rtot); // (barriers inside)
-		lds[L_CHUNK / 4u + tid] = ex;
+		// each thread owns CPT consecutive chunks
+		constexpr uint32_t CPT = PECH_MAX_CHUNKS / PECH_MAIN_THREADS;
+		uint32_t pv[CPT], sum = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < CPT; ++k) {
+			const uint32_t c = tid * CPT + k;
+			pv[k] = c < nchunks ? partials[c] : 0u;
+			lds[L_NZ / 4u + c] = c < nchunks ? nzs[c] : 0u;
+			sum += pv[k];
+		}
+		uint32_t ex = block_excl_scan<PECH_MAIN_THREADS>(sum, lds + L_MISC / 4u, &Rtot); // (barriers inside)
+#pragma unroll
+		for (uint32_t k = 0; k < CPT; ++k) {
+			lds[L_CHUNK / 4u + tid * CPT + k] = ex;
+			ex += pv[k];
+		}
 	}
 	__syncthreads();
 	Rtot = uni(Rtot);
-	const uint64_t W = (uint64_t)gridDim.x * PECH_WAVES_PER_WG;
+	const uint64_t W = (uint64_t)gridDim.x * PECH_MAIN_WAVES;
 	const uint64_t rpw64 = ((uint64_t)Rtot + W - 1) / W;
 	uint32_t rpw = (uint32_t)(rpw64 < rpw_min ? rpw_min : rpw64);
 	if (PECH_ODD_RPW)
 		rpw |= 1u;
-	if ((uint64_t)blockIdx.x * PECH_WAVES_PER_WG * rpw >= Rtot)
+	if ((uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw >= Rtot)
 		return; // whole workgroup idle (small batch)
 
 	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
@@ -575,7 +592,7 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	// same offset modulo the (power-of-two) slice size, which concentrates
 	// requests on few HBM channels (measured on the read probe: 6.66 ->
 	// 7.01 TB/s).  Both starts are found by a 32-ary search each.
-	const uint32_t wid = blockIdx.x * PECH_WAVES_PER_WG + wave;
+	const uint32_t wid = blockIdx.x * PECH_MAIN_WAVES + wave;
 	const uint64_t r0_64 = (uint64_t)wid * rpw;
 	const uint32_t r0 = (uint32_t)min(r0_64, (uint64_t)Rtot);
 	const uint32_t rem_all = (uint32_t)min((uint64_t)rpw, (uint64_t)Rtot - r0);
@@ -601,7 +618,7 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	}
 
 	// stage the tables: A_128 once per bank, the rest single copy
-	for (uint32_t j = tid; j < 8192u; j += PECH_WG_THREADS) {
+	for (uint32_t j = tid; j < 8192u; j += PECH_MAIN_THREADS) {
 		const uint32_t A = j << 4;
 		const uint32_t k = ((A >> 16) << 1) | ((A >> 7) & 1u);
 		const uint32_t v = consts[PECH_C_TAB128 + k * 256u + ((A >> 8) & 0xFFu)];
@@ -609,7 +626,7 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS, 1) void pech_crc32c_mai
 	}
 	{
 		const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
-		for (uint32_t j = tid; j < (PECH_C_TAB1 - PECH_C_TAB4) / 4u; j += PECH_WG_THREADS)
+		for (uint32_t j = tid; j < (PECH_C_TAB1 - PECH_C_TAB4) / 4u; j += PECH_MAIN_THREADS)
 			*(u32x4 *)((char *)lds + L_TAB4 + 16u * j) = c4[j];
 	}
 	__syncthreads();
@@ -690,7 +707,7 @@ extern "C" hipError_t pech_launch_main(const pech_core *cores, uint32_t n, const
 				       uint32_t *out, uint32_t ncu, uint32_t rpw_min, hipStream_t stream)
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
-	hipLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_WG_THREADS), 0, stream, cores, lrs, partials, nzs,
+	hipLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, cores, lrs, partials, nzs,
 			   nch, consts, out, rpw_min);
 	return hipGetLastError();
 }
@@ -699,5 +716,6 @@ extern "C" hipError_t pech_launch_main(const pech_core *cores, uint32_t n, const
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.2 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(PECH_U);
+	return "pech_crc32c 0.3 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }

@@ -23,6 +23,7 @@ def _consts():
         out[m.group(1)] = int(m.group(2))
     ksrc = open(os.path.join(REPO, "pech_amd", "csrc", "crc32c_kernels.hip")).read()
     out["PECH_U"] = int(re.search(r"#define PECH_U (\d+)", ksrc).group(1))
+    out["PECH_MAIN_WAVES"] = int(re.search(r"#define PECH_MAIN_WAVES (\d+)", ksrc).group(1))
     out["PECH_ROTATE"] = int(re.search(r"#define PECH_ROTATE (\d+)", ksrc).group(1))
     out["PECH_ODD_RPW"] = int(re.search(r"#define PECH_ODD_RPW (\d+)", ksrc).group(1))
     return out
@@ -33,7 +34,7 @@ ROW = C["PECH_ROW_BYTES"]
 CHUNK = C["PECH_CHUNK"]
 SPLIT = C["PECH_SPLIT_ROWS"]
 LARGE = C["PECH_LARGE_ROWS"]
-WAVES_PER_WG = C["PECH_WG_THREADS"] // 64
+WAVES_PER_WG = C["PECH_MAIN_WAVES"]
 
 
 def core_rows(addr, ln):
