@@ -27,6 +27,11 @@ asm: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	cd build && $(HIPCC) $(HIPFLAGS) --cuda-device-only -S -Rpass-analysis=kernel-resource-usage \
 		../pech_amd/csrc/crc32c_kernels.hip -o crc32c_kernels.s
 
+# A/B diagnostic build: make variant V=name D="-DPECH_U=9" -> build/lib_name.so
+variant: build/crc32c_api.o
+	$(HIPCC) $(HIPFLAGS) $(D) -c pech_amd/csrc/crc32c_kernels.hip -o build/k_$(V).o
+	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o build/crc32c_api.o
+
 oracle:
 	$(MAKE) -C oracle all
 	@if [ -d /root/reference/include ]; then $(MAKE) -C oracle ref; fi
@@ -35,4 +40,4 @@ clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all asm oracle clean
+.PHONY: all asm variant oracle clean

@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive pinned-host leg")
+    ap.add_argument("--host-passes", type=int, default=4)
     ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
     return ap.parse_args()
 
@@ -164,6 +166,8 @@ def main():
                      "launches": launches},
     }
 
+    if rank == 0 and world == 1 and not args.no_host_path:
+        line["pcie_inclusive"] = host_path(args, bufs[0], offs, sizes, outs, P)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, bufs[0], offs, sizes, outs, rotate, P)
 
@@ -172,6 +176,40 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_path(args, buf0, offs, sizes, outs, P):
+    """PCIe-inclusive rate (reported beside `value`, never as it): the same
+    batch in pinned host memory through crc32c_batch(..., CRC32C_F_PINNED) --
+    hipMemcpyAsync H2D of each buffer (in place, >= 64 KiB) into double-
+    buffered 64 MiB device slots, plan + main kernels, D2H of the results.
+    Outputs are checked bit-exact against the device-resident run."""
+    import torch
+    from pech_amd import _lib
+
+    n = len(sizes)
+    host = torch.empty(int(buf0.numel()), dtype=torch.uint8, pin_memory=True)
+    host.copy_(buf0)
+    P.dev_batch_async(P.make_descs(buf0.data_ptr() + offs, sizes, device=buf0.device), outs[0])
+    torch.cuda.synchronize()
+    want = outs[0].cpu().numpy().view(np.uint32)
+    ptrs = (ctypes.c_void_p * n)(*[host.data_ptr() + int(o) for o in offs])
+    lens = (ctypes.c_uint * n)(*[int(x) for x in sizes])
+    out = (ctypes.c_uint32 * n)()
+    lib = _lib.lib()
+    _lib.check(lib.crc32c_batch(ptrs, lens, None, out, n, P.F_PINNED), "crc32c_batch")  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.host_passes):
+        _lib.check(lib.crc32c_batch(ptrs, lens, None, out, n, P.F_PINNED), "crc32c_batch")
+    dt = time.perf_counter() - t0
+    got = np.frombuffer(out, dtype=np.uint32)
+    if not np.array_equal(got, want):
+        raise SystemExit("PARITY FAILURE: pinned-host path differs from the device-resident path")
+    nbytes = int(sizes.sum())
+    return {"value": round(nbytes * args.host_passes / dt / (1 << 30), 2), "unit": "GiB/s",
+            "path": "crc32c_batch(CRC32C_F_PINNED): pinned host buffers, H2D hipMemcpyAsync into double-buffered "
+                    "64 MiB device slots, plan+main kernels, D2H results; synchronous call",
+            "bytes_per_pass": nbytes, "passes": args.host_passes, "matches_device_path": True}
 
 
 def cpu_baseline(args, buf0, offs, sizes, outs, rotate, P):

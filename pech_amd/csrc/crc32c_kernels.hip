@@ -109,25 +109,32 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_o
 	return *(const uint32_t *)((const char *)lds + byte_off);
 }
 
-// A_128(s) from the bank-replicated tables.  lreg = (lane&31)*4 | 1<<16.
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// A_128(s) ^ w from the bank-replicated tables.  lreg = (lane&31)*4 | 1<<16.
 // Table k, entry e, bank copy c lives at (k>>1)*64K + e*256 + (k&1)*128 + 4c.
-__device__ __forceinline__ uint32_t adv128(const uint32_t *lds, uint32_t s, uint32_t lreg)
+// Five-operand XOR as two bitop3s.
+__device__ __forceinline__ uint32_t adv128(const uint32_t *lds, uint32_t s, uint32_t lreg, uint32_t w)
 {
 #ifdef PECH_AB_NOLDS // diagnostic build only: no table lookups (wrong CRCs)
-	return (s << 1) ^ (s >> 3) ^ lreg;
+	return (s << 1) ^ (s >> 3) ^ lreg ^ w;
 #endif
 	const uint32_t a0 = __builtin_amdgcn_perm(s, lreg, 0x0C0C0400u);
 	const uint32_t a1 = __builtin_amdgcn_perm(s, lreg, 0x0C0C0500u);
 	const uint32_t a2 = __builtin_amdgcn_perm(s, lreg, 0x0C020600u);
 	const uint32_t a3 = __builtin_amdgcn_perm(s, lreg, 0x0C020700u);
-	return lds_u32(lds, a0) ^ lds_u32(lds, a1 + 128u) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3 + 128u);
+	return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1 + 128u), w), lds_u32(lds, a2), lds_u32(lds, a3 + 128u));
 }
 
 // single-copy byte tables (4 x 256 words at byte offset `tab`)
 __device__ __forceinline__ uint32_t adv_tab(const uint32_t *lds, uint32_t tab, uint32_t v)
 {
 	const uint32_t *t = lds + (tab >> 2);
-	return t[v & 0xFFu] ^ t[256u + ((v >> 8) & 0xFFu)] ^ t[512u + ((v >> 16) & 0xFFu)] ^ t[768u + (v >> 24)];
+	return xor3(t[v & 0xFFu], t[256u + ((v >> 8) & 0xFFu)], t[512u + ((v >> 16) & 0xFFu)] ^ t[768u + (v >> 24)]);
 }
 
 // v * x^(8m) mod P with the 64-ary power table POWB[i][j] = x^(8 j 64^i)
@@ -481,30 +488,35 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 #define STEP_ORIG(S) ((S).oz & 0xFFFFFu)
 #define STEP_M(S) ((uint64_t)((S).mp >> 4) * PECH_ROW_BYTES + ((S).mp & 15u))
 
-// first PECH_U rows of a step into the ring (clamped to its rows)
+// Ring discipline: row k of a step lives in ring slot k % PECH_U and the
+// lookahead is PECH_U-1 rows.  The iteration that consumes row k first issues
+// the load of row k+PECH_U-1 into the slot row k-1 has just vacated, so no
+// slot ever holds two live values: the register mapping is static across
+// the loop back-edge (no copies, and no vmcnt(0) drain to make them).
+// Priming loads rows 0..PECH_U-2 (clamped to the step's rows).
 #define RING_PRIME(S, ring)                                                                           \
 	do {                                                                                          \
 		const uint32_t last_ = (S).nl - 1u;                                                   \
-		_Pragma("unroll") for (uint32_t i = 0; i < PECH_U; ++i) (ring)[i] =                   \
+		_Pragma("unroll") for (uint32_t i = 0; i + 1 < PECH_U; ++i) (ring)[i] =               \
 			LD_PIECE((S), row_addr((S).ad, min(i, last_), STEP_ZOFF(S)), 1);                 \
 	} while (0)
 
 __device__ __forceinline__ void horner_row(const uint32_t *lds, uint32_t lreg, u32x4 w, uint32_t &s0, uint32_t &s1,
 					   uint32_t &s2, uint32_t &s3)
 {
-	s0 = adv128(lds, s0, lreg) ^ w.x;
-	s1 = adv128(lds, s1, lreg) ^ w.y;
-	s2 = adv128(lds, s2, lreg) ^ w.z;
-	s3 = adv128(lds, s3, lreg) ^ w.w;
+	s0 = adv128(lds, s0, lreg, w.x);
+	s1 = adv128(lds, s1, lreg, w.y);
+	s2 = adv128(lds, s2, lreg, w.z);
+	s3 = adv128(lds, s3, lreg, w.w);
 }
 
 __device__ __forceinline__ void horner_row_pred(const uint32_t *lds, uint32_t lreg, u32x4 w, bool ok, uint32_t &s0,
 						uint32_t &s1, uint32_t &s2, uint32_t &s3)
 {
-	const uint32_t t0 = adv128(lds, s0, lreg) ^ w.x;
-	const uint32_t t1 = adv128(lds, s1, lreg) ^ w.y;
-	const uint32_t t2 = adv128(lds, s2, lreg) ^ w.z;
-	const uint32_t t3 = adv128(lds, s3, lreg) ^ w.w;
+	const uint32_t t0 = adv128(lds, s0, lreg, w.x);
+	const uint32_t t1 = adv128(lds, s1, lreg, w.y);
+	const uint32_t t2 = adv128(lds, s2, lreg, w.z);
+	const uint32_t t3 = adv128(lds, s3, lreg, w.w);
 	s0 = ok ? t0 : s0;
 	s1 = ok ? t1 : s1;
 	s2 = ok ? t2 : s2;
@@ -618,11 +630,16 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 	}
 
 	// stage the tables: A_128 once per bank, the rest single copy
-	for (uint32_t j = tid; j < 8192u; j += PECH_MAIN_THREADS) {
-		const uint32_t A = j << 4;
-		const uint32_t k = ((A >> 16) << 1) | ((A >> 7) & 1u);
-		const uint32_t v = consts[PECH_C_TAB128 + k * 256u + ((A >> 8) & 0xFFu)];
-		*(u32x4 *)((char *)lds + A) = (u32x4)(v);
+	// (one global load per table word, then its 32 bank copies as 8 x 16 B;
+	// lane t starts at copy group t mod 8 so neighbouring lanes, whose rows
+	// are 256 B apart, write different banks)
+	for (uint32_t t = tid; t < 1024u; t += PECH_MAIN_THREADS) {
+		const uint32_t k = t >> 8, e = t & 0xFFu;
+		const u32x4 v = (u32x4)(consts[PECH_C_TAB128 + t]);
+		char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+#pragma unroll
+		for (uint32_t q = 0; q < 8u; ++q)
+			*(u32x4 *)(dst + 16u * ((q + t) & 7u)) = v;
 	}
 	{
 		const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
@@ -643,12 +660,11 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 		uint32_t blk = 0;
 		// full blocks: every lane's rows valid, prefetch stays inside every run
 		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
-			const uint64_t base = S.ad + (uint64_t)(blk + 1) * U * PECH_ROW_BYTES;
+			const uint64_t base = S.ad + (uint64_t)blk * U * PECH_ROW_BYTES;
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
-				const u32x4 w = ring[i];
-				ring[i] = LD_PIECE(S, base + i * PECH_ROW_BYTES, 2);
-				horner_row(lds, lreg, w, s0, s1, s2, s3);
+				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
+				horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
 			}
 		}
 		// ragged blocks: clamped prefetch, predicated update
@@ -656,25 +672,27 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 			const uint32_t r = blk * U;
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
-				const u32x4 w = ring[i];
-				ring[i] = LD_PIECE(S, row_addr(S.ad, min(r + U + i, last), STEP_ZOFF(S)), 3);
-				horner_row_pred(lds, lreg, w, r + i < S.nu, s0, s1, s2, s3);
+				ring[(i + U - 1) % U] =
+					LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
+				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
 			}
 		}
-		// last block: its loads already fetch the next step's first rows
-		const Step N = plan_step(cores, lds, nx, S.pos, S.lr, S.rem, lane, g8, grp);
+		// last block: its first load is this step's last row, the rest
+		// already fetch the next step's first rows
 		const uint32_t r = blk * U;
+		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
+		const Step N = plan_step(cores, lds, nx, S.pos, S.lr, S.rem, lane, g8, grp);
+		horner_row_pred(lds, lreg, ring[0], r < S.nu, s0, s1, s2, s3);
 		if (N.T) {
 			const uint32_t nlast = N.nl - 1u;
 #pragma unroll
-			for (uint32_t i = 0; i < U; ++i) {
-				const u32x4 w = ring[i];
-				ring[i] = LD_PIECE(N, row_addr(N.ad, min(i, nlast), STEP_ZOFF(N)), 4);
-				horner_row_pred(lds, lreg, w, r + i < S.nu, s0, s1, s2, s3);
+			for (uint32_t i = 1; i < U; ++i) {
+				ring[i - 1] = LD_PIECE(N, row_addr(N.ad, min(i - 1, nlast), STEP_ZOFF(N)), 5);
+				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
 			}
 		} else {
 #pragma unroll
-			for (uint32_t i = 0; i < U; ++i)
+			for (uint32_t i = 1; i < U; ++i)
 				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
 		}
 		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));

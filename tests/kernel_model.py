@@ -94,28 +94,53 @@ def plan(descs, rng=None):
 
 
 def run_rows_loads(U, nl, nu, zoff, T, nmin):
-    """Row indices (and whether the zoff redirect applies) loaded by
-    run_rows for one lane, and the rows it consumes (r < nu)."""
+    """Row indices (and whether the zoff redirect applies) loaded by one
+    lane for one step, in issue order, and the rows it consumes (r < nu).
+
+    Ring discipline of the kernel: row k lives in slot k % U; priming loads
+    rows 0..U-2; the iteration consuming row k first loads row k+U-1 into
+    slot (k-1) % U.  The last block's iterations 1..U-1 load the NEXT step's
+    rows 0..U-2 (modelled as that step's priming).  Slot contents are
+    simulated and every consumed row is checked to be the row in its slot."""
     last = nl - 1
     loads = []
+    slots = {}
 
-    def row_addr(row):
-        loads.append((row, row == 0 and zoff != 0))
+    def load(row, clamp, zo):
+        r = min(row, last) if clamp else row
+        loads.append((r, zo and r == 0 and zoff != 0))
+        slots[row % U] = (row, r)
 
-    for i in range(U):
-        row_addr(min(i, last))
+    for i in range(U - 1):
+        load(i, True, True)
     nblk = (T + U - 1) // U
+    consumed = []
+
+    def consume(k):
+        want, got = slots[k % U]
+        assert want == k, ("ring slot holds row", want, "consuming", k)
+        if k < nu:
+            assert got == k, ("consumed row was clamped", k, got)
+            consumed.append(k)
+
     blk = 0
     while blk + 1 < nblk and (blk + 2) * U <= nmin:
         for i in range(U):
-            loads.append(((blk + 1) * U + i, False))
+            load(blk * U + i + U - 1, False, False)
+            consume(blk * U + i)
         blk += 1
     while blk + 1 < nblk:
         r = blk * U
         for i in range(U):
-            row_addr(min(r + U + i, last))
+            load(r + i + U - 1, True, True)
+            consume(r + i)
         blk += 1
-    consumed = [r for r in range(nblk * U) if r < nu]
+    r = blk * U
+    load(r + U - 1, True, True)
+    consume(r)
+    for i in range(1, U):
+        slots[(i - 1) % U] = ("next step row", i - 1)  # overwritten by the next step's priming
+        consume(r + i)
     return loads, consumed
 
 

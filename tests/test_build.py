@@ -64,3 +64,36 @@ def test_main_kernel_hot_loop_shape(device_asm):
     assert "ds_read_b32" in body and "offset:128" in body
     # the prefetch ring waits are counted, not drained
     assert re.search(r"s_waitcnt vmcnt\([1-9]\d*\)", body)
+    # the five-operand XOR of a Horner step is two v_bitop3_b32
+    assert "v_bitop3_b32" in body
+
+
+def _blocks(body):
+    out, cur = [], None
+    for line in body.split("\n"):
+        m = re.match(r"^(\.LBB\w+):(.*)", line)
+        if m:
+            cur = [m.group(1), [], m.group(2)]
+            out.append(cur)
+        elif cur is not None and line.strip() and not line.strip().startswith(";"):
+            cur[1].append(line.strip())
+    return out
+
+
+def test_row_loops_never_drain_the_ring(device_asm):
+    """The row loops (basic blocks with a full block of Horner steps and
+    their prefetch loads) keep PECH_U-1 loads in flight across the back
+    edge: no vmcnt(0) and no ring-register copies (which is what a ring
+    slot holding two live values compiles to -- found in the ISA of v0.3)."""
+    asm, _ = device_asm
+    body = kernel_body(asm, "pech_crc32c_main")
+    # every block holding a run of Horner steps with their prefetch loads
+    loops = [(n, ins) for n, ins, note in _blocks(body)
+             if sum(i.startswith("v_perm_b32") for i in ins) >= 64
+             and sum(i.startswith("global_load_dwordx4") for i in ins) >= 4]
+    assert len(loops) >= 2, [(n, note) for n, _, note in _blocks(body)]
+    for name, ins in loops:
+        waits = [i for i in ins if "vmcnt(0)" in i]
+        assert not waits, (name, waits)
+        movs = [i for i in ins if i.startswith("v_mov_b32") or i.startswith("v_mov_b64")]
+        assert len(movs) <= 8, (name, len(movs))
