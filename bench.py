@@ -44,6 +44,11 @@ CONFIGS = {
     "c3": ([4 << 20] * 256, 2, "c3: 256 x 4 MiB device-resident buffers per GPU, 2 rotating batches (2 GiB)"),
     "c4": (None, 2, "c4: mixed 4 KiB/64 KiB/1 MiB/4 MiB, equal bytes per class (1 GiB) per GPU, shuffled seed 42, "
                     "2 rotating batches"),
+    # C4's size classes as separate launches (per-size GiB/s), 256 MiB each, 4 rotating batches
+    "c4-4k": ([4096] * 65536, 4, "c4 class 4 KiB: 65,536 x 4 KiB per launch"),
+    "c4-64k": ([65536] * 4096, 4, "c4 class 64 KiB: 4,096 x 64 KiB per launch"),
+    "c4-1m": ([1 << 20] * 256, 4, "c4 class 1 MiB: 256 x 1 MiB per launch"),
+    "c4-4m": ([4 << 20] * 64, 4, "c4 class 4 MiB: 64 x 4 MiB per launch"),
 }
 
 
@@ -128,6 +133,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kernel_ms, launches = P.timing_read()
+    samples = np.asarray(P.timing_samples(), dtype=np.float64) * 1e3  # us per main-kernel launch
     P.timing(False)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -163,6 +169,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "pech_crc32c_main", "avg_launch_us": round(avg_kernel_s * 1e6, 2),
+                     "launch_us_p10_p50_p90": [round(float(np.percentile(samples, q)), 2) for q in (10, 50, 90)]
+                     if len(samples) else None,
                      "launches": launches},
     }
 

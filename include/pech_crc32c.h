@@ -96,6 +96,9 @@ int crc32c_device_init(void);
  * summed kernel milliseconds and launch count since the last read. */
 int crc32c_timing(int enable);
 int crc32c_timing_read(double *kernel_ms, uint64_t *launches);
+/* Per-launch milliseconds collected by the last crc32c_timing_read():
+ * copies up to `max` into `ms`, returns how many there were. */
+int crc32c_timing_samples(float *ms, unsigned int max);
 
 /* Text of the last error (thread-local), "" if none. */
 const char *crc32c_last_error(void);

@@ -39,6 +39,7 @@ SIGNATURES = {
     "crc32c_device_init": (ctypes.c_int, []),
     "crc32c_timing": (ctypes.c_int, [ctypes.c_int]),
     "crc32c_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+    "crc32c_timing_samples": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.c_uint]),
     "crc32c_last_error": (ctypes.c_char_p, []),
     "crc32c_version": (ctypes.c_char_p, []),
 }

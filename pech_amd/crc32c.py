@@ -15,7 +15,7 @@ from ._lib import CDesc, Crc32cError, check, lib
 
 __all__ = [
     "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
-    "crc32c_tensors", "shard_ranges", "Crc32cError", "timing", "timing_read", "version",
+    "crc32c_tensors", "shard_ranges", "Crc32cError", "timing", "timing_read", "timing_samples", "version",
 ]
 
 F_HOST, F_DEVICE, F_PINNED = 0, 1, 2
@@ -141,6 +141,14 @@ def timing_read():
     cnt = ctypes.c_uint64()
     check(lib().crc32c_timing_read(ctypes.byref(ms), ctypes.byref(cnt)), "crc32c_timing_read")
     return ms.value, cnt.value
+
+
+def timing_samples():
+    """Per-launch main-kernel milliseconds gathered by the last timing_read()."""
+    n = lib().crc32c_timing_samples(None, 0)
+    buf = (ctypes.c_float * max(n, 1))()
+    lib().crc32c_timing_samples(buf, n)
+    return list(buf)[:n]
 
 
 def version():

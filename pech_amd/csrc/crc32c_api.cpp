@@ -107,6 +107,7 @@ struct DevCtx {
 static std::mutex g_mu;
 static DevCtx g_ctx[64];
 static bool g_timing = false;
+static std::vector<float> g_samples; // per-launch main-kernel ms of the last timing_read
 static uint32_t g_host_consts[PECH_C_WORDS];
 static bool g_host_consts_ready = false;
 
@@ -536,6 +537,7 @@ int crc32c_timing_read(double *kernel_ms, uint64_t *launches)
 	std::lock_guard<std::mutex> lk(g_mu);
 	double ms = 0;
 	uint64_t cnt = 0;
+	g_samples.clear();
 	for (int d = 0; d < 64; ++d) {
 		DevCtx *c = &g_ctx[d];
 		for (auto &tl : c->pending) {
@@ -544,6 +546,7 @@ int crc32c_timing_read(double *kernel_ms, uint64_t *launches)
 			HIP_TRY(hipEventElapsedTime(&t, tl.a, tl.b));
 			ms += t;
 			++cnt;
+			g_samples.push_back(t);
 			c->free_events.push_back(tl);
 		}
 		c->pending.clear();
@@ -553,6 +556,19 @@ int crc32c_timing_read(double *kernel_ms, uint64_t *launches)
 	if (launches)
 		*launches = cnt;
 	return 0;
+}
+
+int crc32c_timing_samples(float *ms, unsigned int max)
+{
+	std::lock_guard<std::mutex> lk(g_mu);
+	if (!ms && max) {
+		set_err("crc32c_timing_samples: null output");
+		return -EINVAL;
+	}
+	const size_t k = g_samples.size() < max ? g_samples.size() : max;
+	for (size_t i = 0; i < k; ++i)
+		ms[i] = g_samples[i];
+	return (int)g_samples.size();
 }
 
 const char *crc32c_last_error(void)

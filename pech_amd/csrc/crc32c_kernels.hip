@@ -234,12 +234,12 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 }
 
 // ---- main kernel ----------------------------------------------------------
-#ifdef PECH_STAMPS // diagnostic build: per-wave start/end s_memtime stamps
+#ifdef PECH_STAMPS // diagnostic build: per-wave entry/start/end s_memrealtime stamps
 #define PECH_MAX_STAMPS 8192u
-__device__ uint64_t pech_stamps[3 * PECH_MAX_STAMPS];
+__device__ uint64_t pech_stamps[4 * PECH_MAX_STAMPS];
 extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
 {
-	return hipMemcpyFromSymbol(host, HIP_SYMBOL(pech_stamps), sizeof(uint64_t) * 3 * n) == hipSuccess ? 0 : -1;
+	return hipMemcpyFromSymbol(host, HIP_SYMBOL(pech_stamps), sizeof(uint64_t) * 4 * n) == hipSuccess ? 0 : -1;
 }
 #endif
 // A step gives each 8-lane group of a wave one run of rows of one buffer.
@@ -561,6 +561,9 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 	constexpr uint32_t U = PECH_U;
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	const uint32_t tid = threadIdx.x;
+#ifdef PECH_STAMPS
+	const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
 
 	// chunk row offsets, non-empty counts and the batch's total row count
 	uint32_t Rtot;
@@ -702,9 +705,10 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 	if (lane == 0 && wid < PECH_MAX_STAMPS) {
 		uint32_t xcc;
 		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-		pech_stamps[3 * wid] = t_start;
-		pech_stamps[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
-		pech_stamps[3 * wid + 2] = ((uint64_t)blockIdx.x << 8) | (xcc & 0xFu);
+		pech_stamps[4 * wid] = t_start;
+		pech_stamps[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+		pech_stamps[4 * wid + 2] = ((uint64_t)blockIdx.x << 8) | (xcc & 0xFu);
+		pech_stamps[4 * wid + 3] = t_entry;
 	}
 #endif
 }
@@ -734,6 +738,6 @@ extern "C" hipError_t pech_launch_main(const pech_core *cores, uint32_t n, const
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.3 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.4 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }
