@@ -73,7 +73,8 @@ int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, u
 			   void *stream);
 
 /* Workspace the device batch needs for n buffers, and the explicit-workspace
- * form (for concurrent streams or graph capture). */
+ * form (for concurrent streams or graph capture).  d_workspace must be
+ * 256-byte aligned (hipMalloc memory is) and used by one launch at a time. */
 size_t crc32c_dev_workspace_bytes(unsigned int n);
 int crc32c_dev_batch_ws_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n,
 			      void *d_workspace, size_t workspace_bytes, void *stream);

@@ -22,10 +22,10 @@
 static_assert(sizeof(struct crc32c_desc) == sizeof(struct pech_desc), "descriptor ABI");
 static_assert(sizeof(struct crc32c_desc) == 16, "descriptor ABI");
 
-extern "C" hipError_t pech_launch_plan(const pech_desc *, uint32_t, pech_core *, uint32_t *, uint32_t *, uint32_t *,
-				       const uint32_t *, uint32_t *, hipStream_t);
-extern "C" hipError_t pech_launch_main(const pech_core *, uint32_t, const uint32_t *, const uint32_t *,
-				       const uint32_t *, const uint32_t *, uint32_t *, uint32_t, uint32_t, hipStream_t);
+extern "C" hipError_t pech_launch_plan(const pech_desc *, uint32_t, const pech_ws *, const uint32_t *, uint32_t *,
+				       hipStream_t);
+extern "C" hipError_t pech_launch_main(uint32_t, const pech_ws *, const uint32_t *, uint32_t *, uint32_t, uint32_t,
+				       hipStream_t);
 
 extern "C" const char *pech_kernel_tag(void);
 
@@ -151,11 +151,10 @@ static int ctx_get(DevCtx **out)
 	return 0;
 }
 
-// workspace: cores[nch*1024] | lrs[nch*1024] | partials[1024] | nzs[1024]
+// workspace layout: layout.h (pech_ws_carve)
 static size_t ws_bytes_for(unsigned int n)
 {
-	const size_t slots = (size_t)((n + PECH_CHUNK - 1) / PECH_CHUNK) * PECH_CHUNK;
-	return slots * (sizeof(pech_core) + 4u) + 2u * PECH_MAX_CHUNKS * 4u;
+	return pech_ws_bytes(n);
 }
 
 static int ws_reserve(DevCtx *c, unsigned int n)
@@ -183,12 +182,12 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			set_err("workspace too small: %zu < %zu", ws_bytes, ws_bytes_for(m));
 			return -EINVAL;
 		}
-		const size_t slots = (size_t)((m + PECH_CHUNK - 1) / PECH_CHUNK) * PECH_CHUNK;
-		pech_core *cores = (pech_core *)ws;
-		uint32_t *lrs = (uint32_t *)(cores + slots);
-		uint32_t *partials = lrs + slots;
-		uint32_t *nzs = partials + PECH_MAX_CHUNKS;
-		HIP_TRY(pech_launch_plan(d_descs + off, m, cores, lrs, partials, nzs, c->d_consts, d_out + off, stream));
+		if ((uintptr_t)ws & 255u) {
+			set_err("workspace must be 256-byte aligned");
+			return -EINVAL;
+		}
+		const pech_ws w = pech_ws_carve(ws, m);
+		HIP_TRY(pech_launch_plan(d_descs + off, m, &w, c->d_consts, d_out + off, stream));
 		TimedLaunch tl{};
 		if (g_timing) {
 			if (!c->free_events.empty()) {
@@ -200,8 +199,7 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			}
 			HIP_TRY(hipEventRecord(tl.a, stream));
 		}
-		HIP_TRY(pech_launch_main(cores, m, lrs, partials, nzs, c->d_consts, d_out + off, (uint32_t)c->ncu,
-					 PECH_RPW_MIN, stream));
+		HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN, stream));
 		if (g_timing) {
 			HIP_TRY(hipEventRecord(tl.b, stream));
 			c->pending.push_back(tl);

@@ -55,3 +55,13 @@ spread = np.array([max(v) - min(v) for v in per.values()]) / 100
 bmax = np.array([max(v) for v in per.values()]) / 100
 print("per-CU end spread us p50/p90/max: %.1f %.1f %.1f" % (pct(spread,50), pct(spread,90), spread.max()))
 print("per-CU last-wave end us p10/p50/p90: %.1f %.1f %.1f" % (pct(bmax,10), pct(bmax,50), pct(bmax,90)))
+
+# by wave slot inside the workgroup (wid % waves-per-WG): systematic arbitration bias?
+wpg = int(os.environ.get("PECH_WAVES", "16"))
+wid = np.nonzero(ok)[0]
+slot = wid % wpg
+print("end p50 by wave slot (us):", [round(pct(e[slot == k], 50) / 100, 1) for k in range(wpg)])
+print("busy p50 by wave slot (us):", [round(pct((e - s)[slot == k], 50) / 100, 1) for k in range(wpg)])
+out_dir = os.path.join(REPO, "gpurun_out")
+os.makedirs(out_dir, exist_ok=True)
+np.savez(os.path.join(out_dir, f"stamps_{cfg}.npz"), start=s, end=e, entry=ent, tag=tag, wid=wid)
