@@ -43,15 +43,6 @@
 // (wave k of the workgroup runs on SIMD k%4 with rank k/4).  The SIMD issues
 // oldest-first, so with equal shares the youngest waves finish last
 // (measured with -DPECH_STAMPS on C3: ranks 0..3 end at 87/112/140/158 us).
-// Work distribution: every wave first streams PECH_STATIC_PCT % of an equal
-// share of the batch's rows; the rest is taken dynamically in items of at
-// least PECH_ITEM_MIN rows from per-XCD queues (grab()).  100 = fully static.
-#ifndef PECH_STATIC_PCT
-#define PECH_STATIC_PCT 100
-#endif
-#ifndef PECH_ITEM_MIN
-#define PECH_ITEM_MIN 256
-#endif
 #ifndef PECH_SLOT_W0
 #define PECH_SLOT_W0 16
 #endif
@@ -180,8 +171,8 @@ __device__ __forceinline__ uint32_t crc_bytes(const uint32_t *t1, uint32_t crc, 
 
 extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 	const pech_desc *__restrict__ descs, uint32_t n, pech_core *__restrict__ cores, uint32_t *__restrict__ lrs,
-	uint32_t *__restrict__ samp, uint32_t *__restrict__ partials, uint32_t *__restrict__ nzs,
-	uint32_t *__restrict__ queues, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
+	uint32_t *__restrict__ partials, uint32_t *__restrict__ nzs, const uint32_t *__restrict__ consts,
+	uint32_t *__restrict__ out)
 {
 	__shared__ uint32_t t1[256];
 	__shared__ uint32_t powb[384];
@@ -248,14 +239,8 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 	uint32_t total;
 	const uint32_t ex = block_excl_scan(rows_at[tid], scratch, &total);
 	lrs[blockIdx.x * PECH_CHUNK + tid] = ex;
-	// every 32nd scan value: the first level of the main kernel's scalar
-	// search (positions past the chunk's non-empty cores compare high)
-	if ((tid & (PECH_CHUNK / PECH_SAMPLES - 1u)) == 0)
-		samp[blockIdx.x * PECH_SAMPLES + tid / (PECH_CHUNK / PECH_SAMPLES)] = rows_at[tid] ? ex : 0xFFFFFFFFu;
 	if (tid == 0)
 		partials[blockIdx.x] = total;
-	if (blockIdx.x == 0 && tid < PECH_QUEUES)
-		queues[tid * PECH_QSTRIDE] = 0u;
 }
 
 // ---- main kernel ----------------------------------------------------------
@@ -369,93 +354,9 @@ __device__ __forceinline__ uint32_t slot_cw(uint32_t k)
 	return c;
 }
 
-// Locate row r with SCALAR loads only (counted on lgkmcnt, so it can run
-// while the wave's vector prefetch ring is in flight): chunk by binary
-// search of the LDS prefix, then the chunk's 32 samples lrs[32k] (plan
-// kernel), then the 32 scan values of the selected bucket.
-__device__ __forceinline__ void sfind(const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ samp,
-				      const uint32_t *lds, uint32_t nchunks, uint32_t r, uint32_t &pos, uint32_t &lr)
-{
-	uint32_t clo = 0, chi = nchunks;
-	while (chi - clo > 1) {
-		const uint32_t mid = (clo + chi) >> 1;
-		if (uni(lds[L_CHUNK / 4u + mid]) <= r)
-			clo = mid;
-		else
-			chi = mid;
-	}
-	const uint32_t rr = r - uni(lds[L_CHUNK / 4u + clo]);
-	const uint32_t nz = uni(lds[L_NZ / 4u + clo]);
-	constexpr uint32_t B = PECH_CHUNK / PECH_SAMPLES;
-	uint32_t k = 0;
-#pragma unroll
-	for (uint32_t j = 1; j < PECH_SAMPLES; ++j) // samp[0] = 0 <= rr
-		k += samp[clo * PECH_SAMPLES + j] <= rr ? 1u : 0u;
-	const uint32_t q0 = k * B; // chunk-local first position of the bucket
-	uint32_t m = 0, lo = 0;
-#pragma unroll
-	for (uint32_t j = 0; j < B; ++j) {
-		const uint32_t v = lrs[clo * PECH_CHUNK + q0 + j];
-		const bool ok = q0 + j < nz && v <= rr; // a prefix of the bucket (strictly increasing)
-		m += ok ? 1u : 0u;
-		lo = ok ? v : lo;
-	}
-	pos = clo * PECH_CHUNK + q0 + m - 1u;
-	lr = rr - lo;
-}
-
-// Dynamic part of the row space (after every wave's static share): PECH_QUEUES
-// contiguous regions of `item`-row work items, one region per XCD.  A wave
-// takes items from its own XCD's region first, then from the others.
-struct Sched {
-	uint32_t dyn0, qlen, item, rtot, nchunks;
-	uint32_t *queues;
-	const uint32_t *lrs, *samp;
-};
-struct Dyn {
-	uint32_t q, tries; // current queue, queues found empty
-};
-
-// Next work item for the wave: (pos, lr, rem), false when every queue is empty.
-// One SCALAR atomic per attempt (s_atomic_add, lgkmcnt): no vector-queue drain.
-__device__ __forceinline__ bool grab(Dyn &dy, const Sched &sc, const uint32_t *lds, uint32_t &pos, uint32_t &lr,
-				     uint32_t &rem)
-{
-	while (dy.tries < PECH_QUEUES) {
-		uint32_t *qp = sc.queues + PECH_QSTRIDE * dy.q;
-		const uint64_t q0 = (uint64_t)sc.dyn0 + (uint64_t)dy.q * sc.qlen;
-		const uint64_t q1 = min(q0 + sc.qlen, (uint64_t)sc.rtot);
-		const uint32_t nitems = q0 < q1 ? (uint32_t)((q1 - q0 + sc.item - 1u) / sc.item) : 0u;
-		// Counters only grow, so a plain (possibly stale) read that already
-		// shows the queue exhausted is final; only otherwise pay the atomic,
-		// which under contention costs microseconds.
-		uint32_t seen = nitems;
-		if (nitems)
-			asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(seen) : "s"(qp) : "memory");
-		uint32_t it = 0xFFFFFFFFu;
-		if (uni(seen) < nitems) {
-			it = 1u;
-			asm volatile("s_atomic_add %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "+s"(it) : "s"(qp) : "memory");
-		}
-		const uint64_t r = q0 + (uint64_t)uni(it) * sc.item;
-		if (r < q1) {
-			rem = (uint32_t)min((uint64_t)sc.item, q1 - r);
-			sfind(sc.lrs, sc.samp, lds, sc.nchunks, (uint32_t)r, pos, lr);
-			pos = uni(pos);
-			lr = uni(lr);
-			return true;
-		}
-		dy.q = (dy.q + 1u) & (PECH_QUEUES - 1u);
-		++dy.tries;
-	}
-	return false;
-}
-
-// Work out the wave's next step from its cursor (pos, lr, rem); when the
-// cursor is exhausted, take the next dynamic work item.
-__device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const uint32_t *lds, Dyn &dy,
-					  const Sched &sc, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
-					  uint32_t g8, uint32_t grp)
+// Work out the wave's next step from its cursor (pos, lr, rem).
+__device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const uint32_t *lds, uint32_t pos,
+					  uint32_t lr, uint32_t rem, uint32_t lane, uint32_t g8, uint32_t grp)
 {
 	Step S;
 	S.T = 0;
@@ -469,11 +370,8 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 	S.blo = S.bhi = 0;
 #endif
 	for (;;) {
-		if (rem == 0) {
-			if (!grab(dy, sc, lds, pos, lr, rem))
-				break;
-			continue;
-		}
+		if (rem == 0)
+			break;
 		const uint32_t c = pos >> 10;
 		const uint32_t nzc = uni(lds[L_NZ / 4u + c]);
 		if ((pos & 1023u) >= nzc) {
@@ -665,9 +563,8 @@ __device__ __forceinline__ void finish_run(const uint32_t *lds, uint32_t g8, uin
 }
 
 extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_main(
-	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ samp,
-	const uint32_t *__restrict__ partials, const uint32_t *__restrict__ nzs, uint32_t *__restrict__ queues,
-	uint32_t nchunks, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min)
+	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
+	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min)
 {
 	constexpr uint32_t U = PECH_U;
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
@@ -700,43 +597,23 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 	}
 	__syncthreads();
 	Rtot = uni(Rtot);
-	// Static share per wave: PECH_STATIC_PCT % of the equal share (at least
-	// rpw_min rows); the rest of the row space is handed out dynamically
-	// (Sched / grab), so XCDs and CUs that stream faster take more of it.
+	// Every wave gets an equal share of the batch's rows (at least rpw_min).
 	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 	const uint32_t rpw_eq = (uint32_t)(((uint64_t)Rtot + W - 1u) / W);
-	const uint32_t rpw = rpw_eq <= rpw_min ? rpw_min
-					       : max(rpw_min, (uint32_t)((uint64_t)rpw_eq * PECH_STATIC_PCT / 100u));
-	const uint32_t s_end = (uint32_t)min((uint64_t)W * rpw, (uint64_t)Rtot);
-	const uint32_t dyn = Rtot - s_end;
+	const uint32_t rpw = max(rpw_min, rpw_eq);
 	const uint64_t wg0 = (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
-	if (wg0 >= s_end && dyn == 0)
+	if (wg0 >= Rtot)
 		return; // whole workgroup idle (small batch)
 
 	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
 	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
 	const uint32_t wave = uni(tid >> 6);
-	Sched sc;
-	sc.dyn0 = s_end;
-	sc.rtot = Rtot;
-	sc.nchunks = nchunks;
-	sc.qlen = (dyn + PECH_QUEUES - 1u) / PECH_QUEUES;
-	sc.item = max((uint32_t)PECH_ITEM_MIN, (uint32_t)(((uint64_t)dyn + 2ull * W - 1u) / (2ull * W)));
-	sc.queues = queues;
-	sc.lrs = lrs;
-	sc.samp = samp;
-	uint32_t xcc;
-	asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-	Dyn dy = {xcc & (PECH_QUEUES - 1u), 0u};
 	u32x4 ring[U];
 	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
 	// contiguous pieces weighted by age rank (see PECH_SLOT_W*).
-	uint32_t r0 = 0, r1 = 0;
-	if (wg0 < s_end) {
-		const uint32_t wg_rows = (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)s_end - wg0);
-		r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * slot_cw(wave) / slot_cw(PECH_MAIN_WAVES));
-		r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * slot_cw(wave + 1u) / slot_cw(PECH_MAIN_WAVES));
-	}
+	const uint32_t wg_rows = (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * slot_cw(wave) / slot_cw(PECH_MAIN_WAVES));
+	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * slot_cw(wave + 1u) / slot_cw(PECH_MAIN_WAVES));
 	const uint32_t rem_all = r1 - r0;
 	uint32_t p0 = 0, lr0 = 0;
 	if (rem_all) {
@@ -745,7 +622,7 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 		p0 = uni(pos);
 		lr0 = uni(lr);
 	}
-	Step S = plan_step(cores, lds, dy, sc, p0, lr0, rem_all, lane, g8, grp);
+	Step S = plan_step(cores, lds, p0, lr0, rem_all, lane, g8, grp);
 	if (S.T)
 		RING_PRIME(S, ring);
 
@@ -801,7 +678,7 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 		// already fetch the next step's first rows
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
-		const Step N = plan_step(cores, lds, dy, sc, S.pos, S.lr, S.rem, lane, g8, grp);
+		const Step N = plan_step(cores, lds, S.pos, S.lr, S.rem, lane, g8, grp);
 		horner_row_pred(lds, lreg, ring[0], r < S.nu, s0, s1, s2, s3);
 		if (N.T) {
 			const uint32_t nlast = N.nl - 1u;
@@ -837,7 +714,7 @@ extern "C" hipError_t pech_launch_plan(const pech_desc *descs, uint32_t n, const
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
 	hipLaunchKernelGGL(pech_crc32c_plan, dim3(nch), dim3(PECH_WG_THREADS), 0, stream, descs, n, ws->cores, ws->lrs,
-			   ws->samp, ws->partials, ws->nzs, ws->queues, consts, out);
+			   ws->partials, ws->nzs, consts, out);
 	return hipGetLastError();
 }
 
@@ -846,7 +723,7 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
 	hipLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ws->cores, ws->lrs,
-			   ws->samp, ws->partials, ws->nzs, ws->queues, nch, consts, out, rpw_min);
+			   ws->partials, ws->nzs, nch, consts, out, rpw_min);
 	return hipGetLastError();
 }
 
@@ -854,6 +731,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.5 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
-		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " static% " PECH_STR(PECH_STATIC_PCT) " xcd-queues";
+	return "pech_crc32c 0.6 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }

@@ -35,9 +35,6 @@
 #define PECH_RPW_MIN 64u          /* min rows per wave (8 KiB)             */
 #define PECH_LARGE_ROWS 2048u     /* size-class cap for the plan's ordering  */
 #define PECH_SPLIT_ROWS 256u      /* >= this: a buffer is split over 8 groups */
-#define PECH_SAMPLES 32u          /* lrs samples per chunk (scalar search)   */
-#define PECH_QUEUES 8u            /* dynamic work queues, one per XCD        */
-#define PECH_QSTRIDE 64u          /* u32 between queue counters (256 B)      */
 
 /* constants block (u32 words), built on the host, uploaded once per device */
 #define PECH_C_TAB128 0u    /* A_128 byte tables, 4 x 256  (row Horner step)  */
@@ -102,14 +99,12 @@ LAYOUT_FN uint32_t pech_size_class(uint32_t rows)
  * carved in this order (each array 256-byte aligned):
  *   cores    pech_core[slots]        sorted core descriptors per chunk
  *   lrs      u32[slots]              chunk-local exclusive row scan
- *   samp     u32[nch * 32]           lrs[32 k] per chunk (0xFFFFFFFF past nz)
  *   partials u32[PECH_MAX_CHUNKS]    rows per chunk
  *   nzs      u32[PECH_MAX_CHUNKS]    non-empty cores per chunk
- *   queues   u32[8 * 64]             dynamic work-queue counters (zeroed by plan)
  * slots = nch * PECH_CHUNK, nch = ceil(m / PECH_CHUNK). */
 struct pech_ws {
 	struct pech_core *cores;
-	uint32_t *lrs, *samp, *partials, *nzs, *queues;
+	uint32_t *lrs, *partials, *nzs;
 };
 
 static inline size_t pech_ws_align(size_t x) { return (x + 255u) & ~(size_t)255u; }
@@ -118,8 +113,7 @@ static inline size_t pech_ws_bytes(uint32_t m)
 {
 	const size_t nch = (m + PECH_CHUNK - 1u) / PECH_CHUNK, slots = nch * PECH_CHUNK;
 	return pech_ws_align(slots * sizeof(struct pech_core)) + pech_ws_align(slots * 4u) +
-	       pech_ws_align(nch * PECH_SAMPLES * 4u) + 2u * pech_ws_align(PECH_MAX_CHUNKS * 4u) +
-	       pech_ws_align(PECH_QUEUES * PECH_QSTRIDE * 4u);
+	       2u * pech_ws_align(PECH_MAX_CHUNKS * 4u);
 }
 
 static inline struct pech_ws pech_ws_carve(void *base, uint32_t m)
@@ -131,13 +125,9 @@ static inline struct pech_ws pech_ws_carve(void *base, uint32_t m)
 	p += pech_ws_align(slots * sizeof(struct pech_core));
 	w.lrs = (uint32_t *)p;
 	p += pech_ws_align(slots * 4u);
-	w.samp = (uint32_t *)p;
-	p += pech_ws_align(nch * PECH_SAMPLES * 4u);
 	w.partials = (uint32_t *)p;
 	p += pech_ws_align(PECH_MAX_CHUNKS * 4u);
 	w.nzs = (uint32_t *)p;
-	p += pech_ws_align(PECH_MAX_CHUNKS * 4u);
-	w.queues = (uint32_t *)p;
 	return w;
 }
 

@@ -24,8 +24,6 @@ def _consts():
     ksrc = open(os.path.join(REPO, "pech_amd", "csrc", "crc32c_kernels.hip")).read()
     out["PECH_U"] = int(re.search(r"#define PECH_U (\d+)", ksrc).group(1))
     out["PECH_MAIN_WAVES"] = int(re.search(r"#define PECH_MAIN_WAVES (\d+)", ksrc).group(1))
-    out["PECH_STATIC_PCT"] = int(re.search(r"#define PECH_STATIC_PCT (\d+)", ksrc).group(1))
-    out["PECH_ITEM_MIN"] = int(re.search(r"#define PECH_ITEM_MIN (\d+)", ksrc).group(1))
     out["PECH_SLOT_W"] = [int(re.search(r"#define PECH_SLOT_W%d (\d+)" % g, ksrc).group(1)) for g in range(4)]
     return out
 
@@ -92,40 +90,6 @@ def plan(descs, rng=None):
         partials.append(acc)
         nzs.append(len(order))
     return cores, lrs, partials, nzs
-
-
-def samples(lrs, nzs):
-    """Plan kernel's per-chunk sample index: lrs[32 k] (0xFFFFFFFF past nz)."""
-    S, B = C["PECH_SAMPLES"], CHUNK // C["PECH_SAMPLES"]
-    out = []
-    for c, nz in enumerate(nzs):
-        for k in range(S):
-            out.append(lrs[c * CHUNK + k * B] if k * B < nz else 0xFFFFFFFF)
-    return out
-
-
-def sfind(lrs, samp, pref, nzs, r):
-    """Kernel sfind(): chunk by binary search, then samples, then the bucket."""
-    nchunks = len(nzs)
-    clo, chi = 0, nchunks
-    while chi - clo > 1:
-        mid = (clo + chi) >> 1
-        if pref[mid] <= r:
-            clo = mid
-        else:
-            chi = mid
-    rr = r - pref[clo]
-    S, B = C["PECH_SAMPLES"], CHUNK // C["PECH_SAMPLES"]
-    k = sum(1 for j in range(1, S) if samp[clo * S + j] <= rr)
-    q0 = k * B
-    m, lo = 0, 0
-    for j in range(B):
-        v = lrs[clo * CHUNK + q0 + j]
-        if q0 + j < nzs[clo] and v <= rr:
-            m += 1
-            lo = v
-    assert m >= 1
-    return clo * CHUNK + q0 + m - 1, rr - lo
 
 
 def run_rows_loads(U, nl, nu, zoff, T, nmin):
@@ -205,83 +169,40 @@ def slot_cw(k, weights):
     return sum(weights[g] * min(4, max(0, k - 4 * g)) for g in range(4))
 
 
-def schedule(Rtot, ncu, rpw_min=None, weights=None, waves=None, static_pct=None, item_min=None):
-    """Kernel prologue: static (r0, r1) per wave and the dynamic queues
-    [(q0, q1)] with the item size."""
+def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None):
+    """Kernel prologue: [r0, r1) of every wave -- an equal share (at least
+    rpw_min rows) per wave, split inside a workgroup by age-rank weight."""
     rpw_min = rpw_min or C["PECH_RPW_MIN"]
     weights = weights or C["PECH_SLOT_W"]
     waves = waves or WAVES_PER_WG
-    pct = C["PECH_STATIC_PCT"] if static_pct is None else static_pct
-    item_min = item_min or C["PECH_ITEM_MIN"]
     W = ncu * waves
-    rpw_eq = (Rtot + W - 1) // W
-    rpw = rpw_min if rpw_eq <= rpw_min else max(rpw_min, rpw_eq * pct // 100)
-    s_end = min(W * rpw, Rtot)
-    dyn = Rtot - s_end
+    rpw = max(rpw_min, (Rtot + W - 1) // W)
     tot = slot_cw(waves, weights)
-    static = []
+    out = []
     for b in range(ncu):
         wg0 = b * waves * rpw
-        if wg0 >= s_end:
+        if wg0 >= Rtot:
             continue
-        wg_rows = min(waves * rpw, s_end - wg0)
+        wg_rows = min(waves * rpw, Rtot - wg0)
         for w in range(waves):
-            static.append((wg0 + wg_rows * slot_cw(w, weights) // tot,
-                           wg0 + wg_rows * slot_cw(w + 1, weights) // tot))
-    NQ = C["PECH_QUEUES"]
-    qlen = (dyn + NQ - 1) // NQ
-    item = max(item_min, (dyn + 2 * W - 1) // (2 * W))
-    queues = [(s_end + q * qlen, min(s_end + (q + 1) * qlen, Rtot)) for q in range(NQ)]
-    return static, queues, item, W
+            out.append((wg0 + wg_rows * slot_cw(w, weights) // tot,
+                        wg0 + wg_rows * slot_cw(w + 1, weights) // tot))
+    return out
 
 
-def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None, static_pct=None):
-    """Static [r0, r1) of every wave (the dynamic rest is in schedule())."""
-    return schedule(Rtot, ncu, rpw_min, weights, waves, static_pct)[0]
-
-
-def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, rng=None, weights=None, static_pct=None,
-         item_min=None):
+def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
     """Yield events: ("load", buf, lane_piece_addr), ("use", orig, row, g8,
-    virtual) and ("finish", orig, run_end_row, m): every wave's static range,
-    then dynamic items taken from the per-XCD queues in a random interleaving
-    (random XCD per wave, so stealing from other queues is exercised)."""
-    import random as _random
-    rng = rng or _random.Random(0)
+    virtual) and ("finish", orig, run_end_row, m) over every wave's range."""
     U = U or C["PECH_U"]
     pref = [0]
     for p in partials:
         pref.append(pref[-1] + p)
     Rtot = pref[-1]
-    samp = samples(lrs, nzs)
-    static, queues, item, W = schedule(Rtot, ncu, rpw_min, weights, static_pct=static_pct, item_min=item_min)
     events = []
-    for r0, r1 in static:
+    for r0, r1 in wave_ranges(Rtot, ncu, rpw_min, weights):
         if r1 > r0:
             pos, lr = find_start(lrs, pref, nzs, r0, 64)
-            assert (pos, lr) == sfind(lrs, samp, pref, nzs, r0)
             walk(cores, nzs, pos, lr, r1 - r0, U, events)
-    counters = [0] * len(queues)
-    NQ = len(queues)
-    active = [[rng.randrange(NQ), 0] for _ in range(min(W, 64))]  # (queue, tries) per simulated wave
-    while active:
-        i = rng.randrange(len(active))
-        st = active[i]
-        q = st[0]
-        it = counters[q]
-        counters[q] += 1
-        q0, q1 = queues[q]
-        r = q0 + it * item
-        if q0 < q1 and r < q1:
-            rem = min(item, q1 - r)
-            pos, lr = sfind(lrs, samp, pref, nzs, r)
-            assert (pos, lr) == find_start(lrs, pref, nzs, r, 64)
-            walk(cores, nzs, pos, lr, rem, U, events)
-        else:
-            st[0] = (q + 1) % NQ
-            st[1] += 1
-            if st[1] >= NQ:
-                active.pop(i)
     return events
 
 

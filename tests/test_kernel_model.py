@@ -9,11 +9,10 @@ import pytest
 import kernel_model as KM
 
 
-def check(descs, ncu=4, seed=0, weights=None, static_pct=None, item_min=None):
+def check(descs, ncu=4, seed=0, weights=None):
     rng = random.Random(seed)
     cores, lrs, partials, nzs = KM.plan(descs, rng)
-    ev = KM.main(cores, lrs, partials, nzs, ncu, rng=rng, weights=weights, static_pct=static_pct,
-                 item_min=item_min)
+    ev = KM.main(cores, lrs, partials, nzs, ncu, weights=weights)
     used = collections.Counter()
     byorig = {}
     for c in cores:
@@ -82,53 +81,22 @@ def test_one_buffer_many_waves():
     check([(1 << 30, 4 << 20)], ncu=1)
 
 
-@pytest.mark.parametrize("weights,pct,item", [([16, 12, 9, 8], None, None), ([16, 1, 1, 1], 50, 64),
-                                              ([1, 1, 1, 16], 100, None), ([16, 16, 16, 16], 0, 32),
-                                              ([16, 16, 16, 16], 30, 100)])
-def test_weighted_shares_and_dynamic_items(weights, pct, item):
+@pytest.mark.parametrize("weights", [[16, 12, 9, 8], [16, 1, 1, 1], [1, 1, 1, 16]])
+def test_weighted_shares(weights):
     sizes = [4096] * 300 + [300000] * 2 + [100] * 40
     random.Random(5).shuffle(sizes)
     descs, base = [], 1 << 16
     for sz in sizes:
         descs.append((base, sz))
         base += sz + 48
-    check(descs, ncu=3, weights=weights, static_pct=pct, item_min=item)
-
-
-@pytest.mark.parametrize("pct", [0, 50, 100])
-def test_dynamic_many_chunks(pct):
-    descs = [(4096 * (i + 1), 0 if (i // 1024) == 1 else (256 if i % 3 else 5000)) for i in range(3100)]
-    check(descs, ncu=2, static_pct=pct, item_min=40)
-
-
-def test_sfind_matches_find_start():
-    rng = random.Random(9)
-    sizes = [rng.choice([0, 7, 16, 200, 4096, 70000]) for _ in range(2500)]
-    descs, base = [], 1 << 20
-    for sz in sizes:
-        descs.append((base, sz))
-        base += sz + 16
-    cores, lrs, partials, nzs = KM.plan(descs, rng)
-    samp = KM.samples(lrs, nzs)
-    pref = [0]
-    for p in partials:
-        pref.append(pref[-1] + p)
-    for r in [0, 1, pref[-1] - 1] + [rng.randrange(pref[-1]) for _ in range(3000)]:
-        assert KM.sfind(lrs, samp, pref, nzs, r) == KM.find_start(lrs, pref, nzs, r, 64)
+    check(descs, ncu=3, weights=weights)
 
 
 @pytest.mark.parametrize("Rtot", [0, 1, 63, 64, 1000, 65536, 8 << 20])
 @pytest.mark.parametrize("ncu", [1, 7, 256])
-@pytest.mark.parametrize("pct", [0, 50, 100])
-def test_schedule_partitions_row_space(Rtot, ncu, pct):
-    static, queues, item, W = KM.schedule(Rtot, ncu, static_pct=pct)
+def test_wave_ranges_partition_row_space(Rtot, ncu):
     pos = 0
-    for r0, r1 in static:
+    for r0, r1 in KM.wave_ranges(Rtot, ncu):
         assert r0 == pos and r1 >= r0
         pos = r1
-    for q0, q1 in queues:
-        if q1 > q0:
-            assert q0 == pos
-            pos = q1
     assert pos == Rtot
-    assert item >= 1
