@@ -69,6 +69,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive pinned-host leg")
     ap.add_argument("--host-passes", type=int, default=4)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams that consecutive batches alternate over (own workspace each)")
+    ap.add_argument("--pipeline-streams", type=int, default=2,
+                    help="second timed pass with batches alternating over this many streams (0: skip)")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
     ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
     return ap.parse_args()
 
@@ -110,45 +116,66 @@ def main():
         descs.append(P.make_descs(b.data_ptr() + offs, sizes, device=dev))
     outs = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(rotate)]
     assert _lib.lib().crc32c_dev_reserve(n) == 0
-    stream = torch.cuda.current_stream(dev)
+    maxs = max(1, args.streams, args.pipeline_streams)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(maxs - 1)]
+    wsb = P.workspace_bytes(n)
+    wss = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(maxs)]
 
-    def step(i):
-        P.dev_batch_async(descs[i % rotate], outs[i % rotate], stream=stream)
+    def timed(nstreams, steps, warmup):
+        """Warm-up, then `steps` batches bracketed by barrier + synchronize;
+        batch i on stream i % nstreams (own workspace).  A batch's output
+        buffer is only ever written from one stream, so steps never race.
+        Returns (elapsed seconds, max over ranks; per-launch main-kernel us)."""
+        if rotate % nstreams:
+            raise SystemExit(f"{nstreams} streams must divide the {rotate} rotating batches")
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize(dev)
-    P.timing(True)
-    P.timing_read()  # discard warm-up launches
+        def step(i):
+            k = i % nstreams
+            P.dev_batch_ws_async(descs[i % rotate], outs[i % rotate], wss[k], stream=streams[k])
 
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kernel_ms, launches = P.timing_read()
-    samples = np.asarray(P.timing_samples(), dtype=np.float64) * 1e3  # us per main-kernel launch
-    P.timing(False)
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize(dev)
+        P.timing(not args.no_kernel_events)
+        P.timing_read()  # discard warm-up launches
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        P.timing_read()
+        samples = np.asarray(P.timing_samples(), dtype=np.float64) * 1e3  # us per main-kernel launch
+        P.timing(False)
+        if dist is not None:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, samples
+
+    nstreams = max(1, args.streams)
+    elapsed, samples = timed(nstreams, args.steps, args.warmup)
+    launches = len(samples)
+    kernel_ms = float(samples.sum()) / 1e3
 
     total_bytes = batch_bytes * args.steps * world
     value = total_bytes / elapsed / (1 << 30)
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
-    achieved_gbs = batch_bytes / avg_kernel_s / 1e9
+    achieved_gbs = batch_bytes / avg_kernel_s / 1e9 if launches else 0.0
 
+    # HBM bytes per launch from the committed rocprofv3 PMC pass of this
+    # config (tools/pmc_traffic.py: FETCH_SIZE x 2, the gfx950 correction of
+    # MI355X_MICROARCH.md), used only when it was taken on this kernel build.
     traffic = None
-    if args.profile_json and os.path.exists(args.profile_json):
-        prof = json.load(open(args.profile_json))
-        traffic = prof.get("hbm_bytes_per_launch")
+    pj = args.profile_json or os.path.join(REPO, "profiles", "r01", f"{args.config}_traffic.json")
+    if os.path.exists(pj):
+        prof = json.load(open(pj))
+        if prof.get("kernel") == P.version():
+            traffic = prof.get("hbm_bytes_per_launch")
 
     line = {
         "metric": "CRC32C GiB/s on device-resident object buffers (4 KiB–4 MiB), 1/2/4/8 GPUs",
@@ -165,6 +192,7 @@ def main():
         "data": "synthetic (uniform random bytes, torch.randint on device), seed 0 per buffer",
         "config": {"workload": desc, "buffers_per_gpu": n, "bytes_per_gpu_per_step": batch_bytes,
                    "parallelism": f"shard{world} (independent buffers per GPU, no collective)",
+                   "streams": nstreams,
                    "kernel": P.version()},
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -174,6 +202,16 @@ def main():
                      "launches": launches},
     }
 
+    if args.pipeline_streams > 1 and args.pipeline_streams != nstreams:
+        # Same batches, consecutive ones on alternating streams: one batch's
+        # plan kernel, launch boundary, prologue and tail overlap its
+        # neighbour's streaming.  Reported beside `value` (per-launch
+        # durations overlap here, so the roofline comes from the serial pass).
+        pel, psamp = timed(args.pipeline_streams, args.steps, args.warmup)
+        line["pipelined"] = {"streams": args.pipeline_streams,
+                             "value": round(total_bytes / pel / (1 << 30), 2), "unit": "GiB/s",
+                             "ms_per_step": round(pel / args.steps * 1e3, 4),
+                             "avg_launch_us": round(float(psamp.mean()), 2) if len(psamp) else None}
     if rank == 0 and world == 1 and not args.no_host_path:
         line["pcie_inclusive"] = host_path(args, bufs[0], offs, sizes, outs, P)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

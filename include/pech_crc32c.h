@@ -92,9 +92,11 @@ uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 /* Eagerly initialise the current device (tables, streams).  Optional. */
 int crc32c_device_init(void);
 
-/* Kernel timing: when enabled, HIP events bracket every main-kernel launch
- * on its stream; crc32c_timing_read() synchronises on them and returns the
- * summed kernel milliseconds and launch count since the last read. */
+/* Kernel timing: when enabled, every main-kernel launch carries a pair of
+ * HIP events stamped by its own dispatch packet (hipExtLaunchKernel: kernel
+ * start and end on its stream, no launch boundary included);
+ * crc32c_timing_read() synchronises on them and returns the summed kernel
+ * milliseconds and launch count since the last read. */
 int crc32c_timing(int enable);
 int crc32c_timing_read(double *kernel_ms, uint64_t *launches);
 /* Per-launch milliseconds collected by the last crc32c_timing_read():

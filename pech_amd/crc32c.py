@@ -15,7 +15,8 @@ from ._lib import CDesc, Crc32cError, check, lib
 
 __all__ = [
     "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
-    "crc32c_tensors", "shard_ranges", "Crc32cError", "timing", "timing_read", "timing_samples", "version",
+    "dev_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
+    "timing_read", "timing_samples", "version",
 ]
 
 F_HOST, F_DEVICE, F_PINNED = 0, 1, 2
@@ -91,6 +92,26 @@ def dev_batch_async(descs, out, stream=None):
         stream = torch.cuda.current_stream(descs.device)
     check(lib().crc32c_dev_batch_async(descs.data_ptr(), out.data_ptr(), n, stream.cuda_stream),
           "crc32c_dev_batch_async")
+
+
+def workspace_bytes(n):
+    """Device workspace one launch of n buffers needs (crc32c_dev_workspace_bytes)."""
+    return int(lib().crc32c_dev_workspace_bytes(n))
+
+
+def dev_batch_ws_async(descs, out, ws, stream=None):
+    """dev_batch_async with an explicit workspace (uint8 device tensor of at
+    least workspace_bytes(n), 256-byte aligned): one workspace per stream
+    lets independent batches run concurrently on several streams."""
+    import torch
+
+    n = descs.shape[0]
+    if out.numel() < n or out.element_size() != 4:
+        raise ValueError("out must hold n 32-bit words")
+    if stream is None:
+        stream = torch.cuda.current_stream(descs.device)
+    check(lib().crc32c_dev_batch_ws_async(descs.data_ptr(), out.data_ptr(), n, ws.data_ptr(), ws.numel(),
+                                          stream.cuda_stream), "crc32c_dev_batch_ws_async")
 
 
 def crc32c_tensors(tensors, seeds=None, offsets=None, lengths=None):

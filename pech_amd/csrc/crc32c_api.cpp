@@ -25,7 +25,7 @@ static_assert(sizeof(struct crc32c_desc) == 16, "descriptor ABI");
 extern "C" hipError_t pech_launch_plan(const pech_desc *, uint32_t, const pech_ws *, const uint32_t *, uint32_t *,
 				       hipStream_t);
 extern "C" hipError_t pech_launch_main(uint32_t, const pech_ws *, const uint32_t *, uint32_t *, uint32_t, uint32_t,
-				       hipStream_t);
+				       hipStream_t, hipEvent_t, hipEvent_t);
 
 extern "C" const char *pech_kernel_tag(void);
 
@@ -197,13 +197,11 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 				HIP_TRY(hipEventCreate(&tl.a));
 				HIP_TRY(hipEventCreate(&tl.b));
 			}
-			HIP_TRY(hipEventRecord(tl.a, stream));
 		}
-		HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN, stream));
-		if (g_timing) {
-			HIP_TRY(hipEventRecord(tl.b, stream));
+		HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN, stream, tl.a,
+					 tl.b));
+		if (g_timing)
 			c->pending.push_back(tl);
-		}
 	}
 	return 0;
 }

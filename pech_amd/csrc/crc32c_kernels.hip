@@ -26,6 +26,7 @@
 //      At a run's end the 32 stream registers of a group are folded (A_4, then
 //      an A_16/A_32/A_64 butterfly over the 8 lanes), shifted to the buffer's
 //      end (x^(8m), power tables) and xor-ed atomically into out[].
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -246,11 +247,15 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 // ---- main kernel ----------------------------------------------------------
 #ifdef PECH_STAMPS // diagnostic build: per-wave entry/start/end s_memrealtime stamps
 #define PECH_MAX_STAMPS 8192u
-__device__ uint64_t pech_stamps[4 * PECH_MAX_STAMPS];
+#define PECH_NSTAMP 8u // start, end, tag, entry, scan, find, plan, fill
+__device__ uint64_t pech_stamps[PECH_NSTAMP * PECH_MAX_STAMPS];
+#define STAMP(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
 extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
 {
-	return hipMemcpyFromSymbol(host, HIP_SYMBOL(pech_stamps), sizeof(uint64_t) * 4 * n) == hipSuccess ? 0 : -1;
+	return hipMemcpyFromSymbol(host, HIP_SYMBOL(pech_stamps), sizeof(uint64_t) * PECH_NSTAMP * n) == hipSuccess ? 0 : -1;
 }
+#else
+#define STAMP(v)
 #endif
 // A step gives each 8-lane group of a wave one run of rows of one buffer.
 // Per lane: `ad` = address of this lane's piece in the run's first row, `nl`
@@ -340,6 +345,19 @@ __device__ __forceinline__ void find_start(const uint32_t *__restrict__ lrs, con
 	}
 	pos = plo;
 	lr = want ? rr - lrs[plo] : 0u;
+}
+
+// s_setprio takes an immediate: wave-uniform branch over the 4 levels
+__device__ __forceinline__ void set_prio(uint32_t p)
+{
+	if (p == 0)
+		__builtin_amdgcn_s_setprio(0);
+	else if (p == 1)
+		__builtin_amdgcn_s_setprio(1);
+	else if (p == 2)
+		__builtin_amdgcn_s_setprio(2);
+	else
+		__builtin_amdgcn_s_setprio(3);
 }
 
 // Cumulative share weight of the workgroup's waves 0..k-1 (PECH_SLOT_W*).
@@ -569,22 +587,54 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 	constexpr uint32_t U = PECH_U;
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	const uint32_t tid = threadIdx.x;
-#ifdef PECH_STAMPS
-	const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
-#endif
+	STAMP(t_entry);
+
+	// Table constants first: their loads (L2/MALL) overlap the chunk-count
+	// loads below, and the LDS fill is done before the scan's barriers --
+	// issued after the ring prime they would queue behind its HBM loads
+	// (vmcnt is in order; measured 4 us of prologue).
+	static_assert(PECH_MAIN_THREADS == 1024u, "table fill: one A_128 word per thread");
+	constexpr uint32_t NT4 = (PECH_C_TAB1 - PECH_C_TAB4) / 4u; // single-copy tables, 16-B words
+	constexpr uint32_t TPT = (NT4 + PECH_MAIN_THREADS - 1u) / PECH_MAIN_THREADS;
+	const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
+	const uint32_t t128 = consts[PECH_C_TAB128 + tid];
+	u32x4 tv[TPT];
+#pragma unroll
+	for (uint32_t k = 0; k < TPT; ++k)
+		tv[k] = tid + k * PECH_MAIN_THREADS < NT4 ? c4[tid + k * PECH_MAIN_THREADS] : (u32x4)(0u);
 
 	// chunk row offsets, non-empty counts and the batch's total row count
 	uint32_t Rtot;
 	{
 		// each thread owns CPT consecutive chunks
 		constexpr uint32_t CPT = (PECH_MAX_CHUNKS + PECH_MAIN_THREADS - 1) / PECH_MAIN_THREADS;
-		uint32_t pv[CPT], sum = 0;
+		uint32_t pv[CPT], nv[CPT], sum = 0;
 #pragma unroll
 		for (uint32_t k = 0; k < CPT; ++k) {
 			const uint32_t c = tid * CPT + k;
 			pv[k] = c < nchunks ? partials[c] : 0u;
+			nv[k] = c < nchunks ? nzs[c] : 0u;
+		}
+		// A_128 once per bank: its 32 copies as 8 x 16 B; lane t starts at
+		// copy group t mod 8 so neighbouring lanes, whose rows are 256 B
+		// apart, write different banks.  Then the single-copy tables.
+		{
+			const uint32_t k = tid >> 8, e = tid & 0xFFu;
+			const u32x4 v = (u32x4)(t128);
+			char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+#pragma unroll
+			for (uint32_t q = 0; q < 8u; ++q)
+				*(u32x4 *)(dst + 16u * ((q + tid) & 7u)) = v;
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < TPT; ++k)
+			if (tid + k * PECH_MAIN_THREADS < NT4)
+				*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
+#pragma unroll
+		for (uint32_t k = 0; k < CPT; ++k) {
+			const uint32_t c = tid * CPT + k;
 			if (c < PECH_MAX_CHUNKS)
-				lds[L_NZ / 4u + c] = c < nchunks ? nzs[c] : 0u;
+				lds[L_NZ / 4u + c] = nv[k];
 			sum += pv[k];
 		}
 		uint32_t ex = block_excl_scan<PECH_MAIN_THREADS>(sum, lds + L_MISC / 4u, &Rtot); // (barriers inside)
@@ -596,6 +646,7 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 		}
 	}
 	__syncthreads();
+	STAMP(t_scan);
 	Rtot = uni(Rtot);
 	// Every wave gets an equal share of the batch's rows (at least rpw_min).
 	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
@@ -622,31 +673,18 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 		p0 = uni(pos);
 		lr0 = uni(lr);
 	}
+	STAMP(t_find);
 	Step S = plan_step(cores, lds, p0, lr0, rem_all, lane, g8, grp);
+	STAMP(t_plan);
 	if (S.T)
 		RING_PRIME(S, ring);
 
-	// stage the tables: A_128 once per bank, the rest single copy
-	// (one global load per table word, then its 32 bank copies as 8 x 16 B;
-	// lane t starts at copy group t mod 8 so neighbouring lanes, whose rows
-	// are 256 B apart, write different banks)
-	for (uint32_t t = tid; t < 1024u; t += PECH_MAIN_THREADS) {
-		const uint32_t k = t >> 8, e = t & 0xFFu;
-		const u32x4 v = (u32x4)(consts[PECH_C_TAB128 + t]);
-		char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
-#pragma unroll
-		for (uint32_t q = 0; q < 8u; ++q)
-			*(u32x4 *)(dst + 16u * ((q + t) & 7u)) = v;
-	}
-	{
-		const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
-		for (uint32_t j = tid; j < (PECH_C_TAB1 - PECH_C_TAB4) / 4u; j += PECH_MAIN_THREADS)
-			*(u32x4 *)((char *)lds + L_TAB4 + 16u * j) = c4[j];
-	}
-	__syncthreads();
+	STAMP(t_fill);
+	__syncthreads(); // tables (written before the scan) and the ring prime
 
-#ifdef PECH_STAMPS
-	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	STAMP(t_start);
+#ifdef PECH_PRIO_YOUNG // diagnostic: younger waves (higher age rank on the SIMD) issue first
+	set_prio(wave >> 2);
 #endif
 	while (S.T) {
 		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -658,6 +696,9 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 		// full blocks: every lane's rows valid, prefetch stays inside every run
 		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
 			const uint64_t base = S.ad + (uint64_t)blk * U * PECH_ROW_BYTES;
+#ifdef PECH_PRIO_ROTATE // diagnostic: rotate issue priority among the SIMD's waves every block
+			set_prio((blk + (wave >> 2)) & 3u);
+#endif
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
@@ -700,10 +741,15 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 	if (lane == 0 && wid < PECH_MAX_STAMPS) {
 		uint32_t xcc;
 		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-		pech_stamps[4 * wid] = t_start;
-		pech_stamps[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
-		pech_stamps[4 * wid + 2] = ((uint64_t)blockIdx.x << 8) | (xcc & 0xFu);
-		pech_stamps[4 * wid + 3] = t_entry;
+		uint64_t *st = pech_stamps + PECH_NSTAMP * wid;
+		st[0] = t_start;
+		st[1] = __builtin_amdgcn_s_memrealtime();
+		st[2] = ((uint64_t)blockIdx.x << 8) | (xcc & 0xFu);
+		st[3] = t_entry;
+		st[4] = t_scan;
+		st[5] = t_find;
+		st[6] = t_plan;
+		st[7] = t_fill;
 	}
 #endif
 }
@@ -718,12 +764,17 @@ extern "C" hipError_t pech_launch_plan(const pech_desc *descs, uint32_t n, const
 	return hipGetLastError();
 }
 
+// ev_start/ev_stop (optional): stamped by the kernel's own dispatch packet
+// (hipExtLaunchKernel), so their interval is the kernel's execution alone,
+// as rocprofv3's kernel trace reports it -- no launch boundary included.
 extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint32_t *consts, uint32_t *out,
-				       uint32_t ncu, uint32_t rpw_min, hipStream_t stream)
+				       uint32_t ncu, uint32_t rpw_min, hipStream_t stream, hipEvent_t ev_start,
+				       hipEvent_t ev_stop)
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
-	hipLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ws->cores, ws->lrs,
-			   ws->partials, ws->nzs, nch, consts, out, rpw_min);
+	hipExtLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u,
+			      (const pech_core *)ws->cores, (const uint32_t *)ws->lrs, (const uint32_t *)ws->partials,
+			      (const uint32_t *)ws->nzs, nch, consts, out, rpw_min);
 	return hipGetLastError();
 }
 

@@ -268,6 +268,30 @@ def test_batch_host_pinned_device_flags(torch_dev, P):
     assert L.crc32c_batch(ptrs, cl, cs, out, n, 3) < 0
 
 
+def test_concurrent_streams_explicit_workspaces(torch_dev, P):
+    # bench.py's pipelined pass: independent batches alternate over streams,
+    # one workspace per stream, launches overlapping on the device
+    torch, dev = torch_dev
+    shapes = [([4096] * 8192, 0), ([4 << 20] * 16, 1), ([65536] * 512, 0xFFFFFFFF), ([1 << 20] * 32, 5)]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    wss = [torch.empty(P.workspace_bytes(8192), dtype=torch.uint8, device=dev) for _ in range(2)]
+    jobs = []
+    for sizes, seed in shapes:
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+        buf = torch.randint(0, 256, (int(np.sum(sizes)),), dtype=torch.uint8, device=dev)
+        descs = P.make_descs(buf.data_ptr() + offs, sizes, [seed] * len(sizes), device=dev)
+        out = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
+        jobs.append((buf, offs, sizes, seed, descs, out))
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i, (_, _, _, _, descs, out) in enumerate(jobs):
+            P.dev_batch_ws_async(descs, out, wss[i % 2], stream=streams[i % 2])
+    torch.cuda.synchronize()
+    for buf, offs, sizes, seed, _, out in jobs:
+        want = O.crcs(buf.cpu().numpy(), offs, sizes, [seed] * len(sizes))
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
 def test_graph_capture_and_replay(torch_dev, P):
     # the device batch enqueues no host sync / allocation: capturable
     torch, dev = torch_dev

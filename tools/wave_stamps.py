@@ -23,21 +23,27 @@ torch.cuda.synchronize()
 L = _lib.lib()
 L.pech_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 W = 4096
-st = np.zeros(4 * W, dtype=np.uint64)
+NS = 8
+st = np.zeros(NS * W, dtype=np.uint64)
 assert L.pech_read_stamps(st.ctypes.data, W) == 0
-s, e, tag, ent = (st[k::4].astype(np.int64) for k in range(4))
+s, e, tag, ent, tscan, tfind, tplan, tfill = (st[k::NS].astype(np.int64) for k in range(NS))
 ok = (s > 0) & (e > 0)
 s, e, tag, ent = s[ok], e[ok], tag[ok], ent[ok]
+tscan, tfind, tplan, tfill = tscan[ok], tfind[ok], tplan[ok], tfill[ok]
 xcc, blk = tag & 0xF, tag >> 8
 # s_memrealtime: 100 MHz chip-wide clock (10 ns ticks)
 t0 = ent.min()
-s -= t0; e -= t0; ent -= t0
+s -= t0; e -= t0; ent -= t0; tscan -= t0; tfind -= t0; tplan -= t0; tfill -= t0
 pro = s - ent
 span = e.max()
 pct = lambda a, q: float(np.percentile(a, q))
 print(f"{cfg}: waves {ok.sum()}, span {span*10/1000:.1f} us")
 print("entry us p50/p99/max: %.1f %.1f %.1f" % (pct(ent,50)/100, pct(ent,99)/100, ent.max()/100))
 print("prologue (entry->first row) us p10/p50/p90/max: %.1f %.1f %.1f %.1f" % (pct(pro,10)/100, pct(pro,50)/100, pct(pro,90)/100, pro.max()/100))
+for nm, a, b in (("entry->scan", ent, tscan), ("scan->find", tscan, tfind), ("find->plan", tfind, tplan),
+                 ("plan->fill", tplan, tfill), ("fill->start(barrier)", tfill, s)):
+    d = b - a
+    print("  %-22s us p10/p50/p90: %.2f %.2f %.2f" % (nm, pct(d, 10) / 100, pct(d, 50) / 100, pct(d, 90) / 100))
 print("start us p50/p99/max: %.1f %.1f %.1f" % (pct(s,50)/100, pct(s,99)/100, s.max()/100))
 print("end   us p1/p10/p50/p90/max: %.1f %.1f %.1f %.1f %.1f" % (pct(e,1)/100, pct(e,10)/100, pct(e,50)/100, pct(e,90)/100, e.max()/100))
 print("mean wave busy / span: %.3f" % float(((e - s) / span).mean()))
