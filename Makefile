@@ -3,18 +3,23 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
-SRC = pech_amd/csrc/crc32c_kernels.hip pech_amd/csrc/crc32c_api.cpp
-HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h include/crc32c.h include/pech_crc32c.h
+SRC = pech_amd/csrc/crc32c_kernels.hip pech_amd/csrc/crc32c_api.cpp pech_amd/csrc/crc32c_async.cpp
+HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h pech_amd/csrc/api_internal.h include/crc32c.h include/pech_crc32c.h \
+      include/pech_crc32c_async.h
 LIB = pech_amd/libpech_crc32c.so
-OBJ = build/crc32c_kernels.o build/crc32c_api.o
+OBJ = build/crc32c_kernels.o build/crc32c_api.o build/crc32c_async.o
 
-all: $(LIB) oracle
+all: $(LIB) oracle build/msgr_sim
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 build/crc32c_api.o: pech_amd/csrc/crc32c_api.cpp $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+build/crc32c_async.o: pech_amd/csrc/crc32c_async.cpp $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
@@ -28,9 +33,16 @@ asm: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 		../pech_amd/csrc/crc32c_kernels.hip -o crc32c_kernels.s
 
 # A/B diagnostic build: make variant V=name D="-DPECH_U=9" -> build/lib_name.so
-variant: build/crc32c_api.o
+variant: build/crc32c_api.o build/crc32c_async.o
 	$(HIPCC) $(HIPFLAGS) $(D) -c pech_amd/csrc/crc32c_kernels.hip -o build/k_$(V).o
-	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o build/crc32c_api.o
+	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o build/crc32c_api.o build/crc32c_async.o
+
+# test program: pech's receive path on the async layer (gnu89, epoll loop);
+# links the test oracle for the expected footer CRCs -- not product code
+build/msgr_sim: tests/c/msgr_sim.c oracle/crc32c_oracle.c include/pech_crc32c_async.h $(LIB)
+	@mkdir -p build
+	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude tests/c/msgr_sim.c oracle/crc32c_oracle.c \
+		-Lpech_amd -lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
 
 oracle:
 	$(MAKE) -C oracle all

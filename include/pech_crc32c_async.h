@@ -1,0 +1,120 @@
+/*
+ * pech_crc32c_async.h -- the messenger-facing layer of libpech_crc32c.so
+ * (SURVEY.md §8f rows 1-3): payload checksums that complete through an
+ * eventfd on pech's epoll loop, DMA-able payload pages, and CRC reuse by
+ * concatenation.  Every result equals the reference's
+ * crc32c(seed, buf, len) (/root/reference/include/crc32c.h:88-96).
+ *
+ * Reference interfaces these serve (file:line in /root/reference):
+ *   crc32c_async_*  -- replaces the per-<=4 KiB-piece ceph_crc32c_iov() chain
+ *                      (src/ceph/messenger.c:1734-1740) of read_partial_msg_data
+ *                      (:2649-2684, verified at the footer :2836-2842) and
+ *                      write_partial_message_data (:1748-1803) with ONE
+ *                      submission per completed payload; completion is an
+ *                      eventfd an event_item watches (include/event.h:7-28),
+ *                      so the single-threaded loop never blocks on the GPU.
+ *   crc32c_pages_*  -- alloc_pages()/__free_pages() (src/page.c:73-146):
+ *                      same 2^order-page sizes and per-order free lists
+ *                      (orders 0..11, 32 MiB cached per order), but pinned,
+ *                      GPU-mapped host memory, so payload bytes received into
+ *                      them reach the GPU by DMA (or are read by the kernel
+ *                      in place) with no staging copy.  Backs alloc_bvec() in
+ *                      osds_alloc_msg() (src/ceph/osd_server.c:2317-2381).
+ *   crc32c_concat   -- the data CRC of a message whose data section is a
+ *                      concatenation of already-checksummed segments: the
+ *                      REPOP fan-out re-sends the request's op data through
+ *                      nested cursors (osd_server.c:1119, sent per replica
+ *                      at :1972) and would otherwise re-scan the same bytes
+ *                      once per replica.
+ *
+ * Threading: an async context belongs to ONE caller thread (pech has one,
+ * README:11-16).  The HIP runtime signals the eventfd from its own thread;
+ * callbacks only ever run inside crc32c_async_complete() on the caller's
+ * thread.  Errors: 0 or a negative errno (include/err.h style), as in
+ * pech_crc32c.h; no CPU fallback.
+ */
+#ifndef PECH_CRC32C_ASYNC_H
+#define PECH_CRC32C_ASYNC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pech_crc32c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- DMA-able payload pages (src/page.c:73-146) ------------------------ */
+#define CRC32C_PAGE_SHIFT 12u
+#define CRC32C_PAGE_SIZE (1u << CRC32C_PAGE_SHIFT)
+#define CRC32C_PAGES_MAX_ORDER 11u /* src/page.c:5; larger orders are not cached */
+
+/* (4096 << order) bytes of pinned, GPU-mapped host memory, page aligned;
+ * NULL on failure (crc32c_last_error()).  Orders <= 11 come from a free list
+ * when one is cached. */
+void *crc32c_pages_alloc(unsigned int order);
+/* Return pages from crc32c_pages_alloc(order); cached up to 32 MiB per order
+ * (src/page.c:6), released to the driver beyond that. */
+void crc32c_pages_free(void *pages, unsigned int order);
+/* 1 if [p, p + len) lies inside ONE live crc32c_pages_alloc() allocation. */
+int crc32c_pages_is_pinned(const void *p, size_t len);
+/* Release every cached free page (deinit_pages(), src/page.c:46-58). */
+void crc32c_pages_trim(void);
+
+/* ---- asynchronous payload checksums ------------------------------------ */
+struct crc32c_async;
+
+/* Completion callback: crc = crc32c(seed, buf, len) of the submission, or
+ * err < 0 if the GPU work failed (crc is then 0 and must not be used). */
+typedef void (*crc32c_done_fn)(void *arg, uint32_t crc, int err);
+
+/* flags for crc32c_async_create() */
+#define CRC32C_ASYNC_DEFAULT 0u
+/* payloads in crc32c_pages memory are read by the kernel in place over the
+ * host link (no H2D copy); without it they are DMA'd to device slots */
+#define CRC32C_ASYNC_ZEROCOPY 1u
+
+/* A context on the current device: its own HIP stream, staging slots and
+ * eventfd.  NULL on failure. */
+struct crc32c_async *crc32c_async_create(unsigned int flags);
+
+/* The eventfd (EFD_NONBLOCK | EFD_CLOEXEC): readable while finished batches
+ * wait for crc32c_async_complete().  Owned by the context. */
+int crc32c_async_fd(const struct crc32c_async *a);
+
+/* Queue crc32c(seed, buf, len) of HOST memory `buf` (pageable, or
+ * crc32c_pages memory: DMA'd or read in place, no CPU copy).  The caller
+ * keeps `buf` unchanged and alive until `done` runs (hold a ceph_msg_get()
+ * reference, messenger.c:3907-3924).  Any length < 2^32, including 0.  A
+ * full batch is launched automatically; otherwise call crc32c_async_flush(). */
+int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsigned int len, uint32_t seed,
+			crc32c_done_fn done, void *arg);
+
+/* Launch everything queued (asynchronous; returns at once). */
+int crc32c_async_flush(struct crc32c_async *a);
+
+/* Run the callbacks of every finished batch, in submission order, on the
+ * calling thread; clears the eventfd.  Returns the number of callbacks run
+ * (>= 0) or a negative errno.  Never blocks. */
+int crc32c_async_complete(struct crc32c_async *a);
+
+/* Flush and wait until every submission's callback has run (shutdown, tests). */
+int crc32c_async_drain(struct crc32c_async *a);
+
+/* Submissions queued or in flight whose callbacks have not run yet. */
+unsigned int crc32c_async_pending(const struct crc32c_async *a);
+
+/* Drain, then free the context (its eventfd is closed). */
+void crc32c_async_destroy(struct crc32c_async *a);
+
+/* ---- CRC reuse by concatenation (host algebra, no data pass) ----------- */
+/* crc32c(seed, S_0 || S_1 || ... || S_{n-1}) from the segments' zero-seeded
+ * CRCs crcs[i] = crc32c(0, S_i, lens[i]).  n == 0 returns seed. */
+uint32_t crc32c_concat(uint32_t seed, const uint32_t *crcs, const uint64_t *lens, unsigned int n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PECH_CRC32C_ASYNC_H */

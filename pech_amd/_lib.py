@@ -23,6 +23,9 @@ class CDesc(ctypes.Structure):
     _fields_ = [("addr", ctypes.c_uint64), ("len", ctypes.c_uint32), ("seed", ctypes.c_uint32)]
 
 
+# completion callback of include/pech_crc32c_async.h: (arg, crc, err)
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int)
+
 # name -> (restype, argtypes); must cover every function in include/*.h
 SIGNATURES = {
     "crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint]),
@@ -41,6 +44,22 @@ SIGNATURES = {
     "crc32c_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
     "crc32c_timing_samples": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.c_uint]),
     "crc32c_last_error": (ctypes.c_char_p, []),
+    # include/pech_crc32c_async.h
+    "crc32c_pages_alloc": (ctypes.c_void_p, [ctypes.c_uint]),
+    "crc32c_pages_free": (None, [ctypes.c_void_p, ctypes.c_uint]),
+    "crc32c_pages_is_pinned": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "crc32c_pages_trim": (None, []),
+    "crc32c_async_create": (ctypes.c_void_p, [ctypes.c_uint]),
+    "crc32c_async_fd": (ctypes.c_int, [ctypes.c_void_p]),
+    "crc32c_async_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint32,
+                                           DONE_FN, ctypes.c_void_p]),
+    "crc32c_async_flush": (ctypes.c_int, [ctypes.c_void_p]),
+    "crc32c_async_complete": (ctypes.c_int, [ctypes.c_void_p]),
+    "crc32c_async_drain": (ctypes.c_int, [ctypes.c_void_p]),
+    "crc32c_async_pending": (ctypes.c_uint, [ctypes.c_void_p]),
+    "crc32c_async_destroy": (None, [ctypes.c_void_p]),
+    "crc32c_concat": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint]),
     "crc32c_version": (ctypes.c_char_p, []),
 }
 

@@ -16,7 +16,7 @@ from ._lib import CDesc, Crc32cError, check, lib
 __all__ = [
     "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
     "dev_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
-    "timing_read", "timing_samples", "version",
+    "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc",
 ]
 
 F_HOST, F_DEVICE, F_PINNED = 0, 1, 2
@@ -174,3 +174,84 @@ def timing_samples():
 
 def version():
     return lib().crc32c_version().decode()
+
+
+def crc32c_concat(seed, crcs, lens):
+    """crc32c(seed, S_0 || ... || S_n-1) from zero-seeded segment CRCs
+    (include/pech_crc32c_async.h; host algebra, no data pass)."""
+    n = len(crcs)
+    c = (ctypes.c_uint32 * max(n, 1))(*[int(x) & 0xFFFFFFFF for x in crcs])
+    l = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in lens])
+    return lib().crc32c_concat(seed & 0xFFFFFFFF, c, l, n)
+
+
+class Pages:
+    """crc32c_pages_alloc(order) memory (pinned, GPU-mapped host pages) as a
+    writable numpy uint8 view; free() returns it to the per-order cache."""
+
+    def __init__(self, order):
+        self.order = order
+        self.nbytes = 4096 << order
+        self.ptr = lib().crc32c_pages_alloc(order)
+        if not self.ptr:
+            raise Crc32cError(f"crc32c_pages_alloc({order}) failed: {lib().crc32c_last_error().decode()}")
+        self.view = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            lib().crc32c_pages_free(self.ptr, self.order)
+            self.ptr = None
+            self.view = None
+
+
+class AsyncCrc:
+    """crc32c_async context (include/pech_crc32c_async.h): submit host
+    payloads, poll fd() from an event loop, complete() runs the callbacks."""
+
+    def __init__(self, zerocopy=False):
+        from ._lib import DONE_FN
+
+        self._h = lib().crc32c_async_create(1 if zerocopy else 0)
+        if not self._h:
+            raise Crc32cError(f"crc32c_async_create failed: {lib().crc32c_last_error().decode()}")
+        self._keep = {}  # submission key -> (payload ref, python callback)
+        self._next = 0
+
+        def trampoline(arg, crc, err):
+            ref, cb = self._keep.pop(arg)
+            cb(crc, err)
+
+        self._cfn = DONE_FN(trampoline)
+
+    def fd(self):
+        return lib().crc32c_async_fd(self._h)
+
+    def submit(self, buf, length, seed, callback, keep=None):
+        """buf: integer address of host bytes; callback(crc, err)."""
+        self._next += 1
+        key = self._next
+        self._keep[key] = (keep, callback)
+        rc = lib().crc32c_async_submit(self._h, buf, length, seed & 0xFFFFFFFF, self._cfn, key)
+        if rc:
+            self._keep.pop(key, None)
+            check(rc, "crc32c_async_submit")
+
+    def flush(self):
+        check(lib().crc32c_async_flush(self._h), "crc32c_async_flush")
+
+    def complete(self):
+        rc = lib().crc32c_async_complete(self._h)
+        if rc < 0:
+            check(rc, "crc32c_async_complete")
+        return rc
+
+    def drain(self):
+        check(lib().crc32c_async_drain(self._h), "crc32c_async_drain")
+
+    def pending(self):
+        return lib().crc32c_async_pending(self._h)
+
+    def close(self):
+        if self._h:
+            lib().crc32c_async_destroy(self._h)
+            self._h = None

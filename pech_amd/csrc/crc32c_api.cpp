@@ -207,6 +207,29 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 }
 
 // ---------------------------------------------------------------------------
+// internal entry points for crc32c_async.cpp (hidden: not part of the C-ABI)
+#include "api_internal.h"
+
+PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
+				     size_t ws_bytes, hipStream_t stream)
+{
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (rc)
+		return rc;
+	return launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream);
+}
+
+PECH_HIDDEN void pech_internal_set_err(const char *fmt, ...)
+{
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(g_err, sizeof(g_err), fmt, ap);
+	va_end(ap);
+}
+
+// ---------------------------------------------------------------------------
 // host staging: two slots of `bytes` pinned host + device memory each
 static int stage_reserve(DevCtx *c, size_t bytes, uint32_t ndesc)
 {
@@ -512,6 +535,16 @@ uint32_t crc32c_shift(uint32_t v, uint64_t nbytes)
 uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b)
 {
 	return gf2_shift(crc_a, len_b) ^ crc_b;
+}
+
+// crc32c(seed, S_0 || ... || S_{n-1}) = A_L(seed) ^ XOR_i A_{after_i}(crc_i),
+// folded left to right: acc <- A_|S_i|(acc) ^ crc_i (Horner over segments)
+uint32_t crc32c_concat(uint32_t seed, const uint32_t *crcs, const uint64_t *lens, unsigned int n)
+{
+	uint32_t acc = seed;
+	for (unsigned int i = 0; i < n; ++i)
+		acc = gf2_shift(acc, lens[i]) ^ crcs[i];
+	return acc;
 }
 
 int crc32c_device_init(void)

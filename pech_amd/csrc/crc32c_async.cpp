@@ -1,0 +1,511 @@
+// crc32c_async.cpp -- the messenger-facing layer (include/pech_crc32c_async.h):
+// pinned payload pages, eventfd-completed payload batches, concatenation.
+//
+// Data path of one async context (one HIP stream):
+//   submit()   places the payload in the slot being filled -- pageable bytes
+//              are packed into the slot's pinned staging buffer (one CPU
+//              copy), crc32c_pages bytes are DMA'd straight from where they
+//              lie (or, with CRC32C_ASYNC_ZEROCOPY, read by the kernel in
+//              place over the host link) -- and records one descriptor per
+//              piece.  A payload larger than what a slot has left is cut
+//              into pieces; piece 0 carries the seed, later pieces seed 0.
+//   flush()    H2D of the packed staging runs and the descriptors, plan +
+//              main kernels, D2H of the results, an event, and a host
+//              function that bumps the eventfd.
+//   complete() harvests finished slots in launch order, folds each piece
+//              into its payload (crc <- crc32c_combine(crc, piece, len)),
+//              frees the slot, and runs the callbacks of finished payloads
+//              in submission order on the caller's thread.
+// No byte is checksummed on the CPU: pieces and combine are GF(2) algebra
+// on kernel results (gf2.h).
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
+
+#include <deque>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "../../include/pech_crc32c_async.h"
+#include "api_internal.h"
+#include "gf2.h"
+#include "layout.h"
+
+#define TRY_HIP(expr, ret)                                                                              \
+	do {                                                                                            \
+		hipError_t e_ = (expr);                                                                 \
+		if (e_ != hipSuccess) {                                                                 \
+			pech_internal_set_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+					      __LINE__);                                                \
+			return ret;                                                                     \
+		}                                                                                       \
+	} while (0)
+
+// ===========================================================================
+// pinned payload pages (src/page.c:73-146 semantics, pinned + GPU-mapped)
+namespace {
+
+struct PageAlloc {
+	size_t bytes;
+	void *dev; // device address of the mapping (hipHostGetDevicePointer)
+	bool live; // handed out (not on a free list)
+};
+
+constexpr unsigned kMaxOrder = CRC32C_PAGES_MAX_ORDER;
+constexpr size_t kMaxCachedPerOrder = 32u << 20; // src/page.c:6
+
+std::mutex g_pages_mu;
+std::map<uintptr_t, PageAlloc> g_pages;          // every pinned allocation, by base
+std::vector<void *> g_free[kMaxOrder + 1];       // cached free allocations per order
+
+// [p, p+len) inside one live allocation: its entry, else end()
+std::map<uintptr_t, PageAlloc>::iterator find_live(const void *p, size_t len)
+{
+	const uintptr_t a = (uintptr_t)p;
+	auto it = g_pages.upper_bound(a);
+	if (it == g_pages.begin())
+		return g_pages.end();
+	--it;
+	if (!it->second.live || a + len > it->first + it->second.bytes || a + len < a)
+		return g_pages.end();
+	return it;
+}
+
+} // namespace
+
+extern "C" void *crc32c_pages_alloc(unsigned int order)
+{
+	if (order > 31u - CRC32C_PAGE_SHIFT) {
+		pech_internal_set_err("crc32c_pages_alloc: order %u too large", order);
+		return nullptr;
+	}
+	const size_t bytes = (size_t)CRC32C_PAGE_SIZE << order;
+	std::lock_guard<std::mutex> lk(g_pages_mu);
+	if (order <= kMaxOrder && !g_free[order].empty()) {
+		void *p = g_free[order].back();
+		g_free[order].pop_back();
+		g_pages[(uintptr_t)p].live = true;
+		return p;
+	}
+	void *p = nullptr;
+	TRY_HIP(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable), nullptr);
+	void *d = nullptr;
+	if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d)
+		d = p; // unified addressing: the host address is the device address
+	g_pages[(uintptr_t)p] = PageAlloc{bytes, d, true};
+	return p;
+}
+
+extern "C" void crc32c_pages_free(void *pages, unsigned int order)
+{
+	if (!pages)
+		return;
+	std::lock_guard<std::mutex> lk(g_pages_mu);
+	auto it = g_pages.find((uintptr_t)pages);
+	if (it == g_pages.end() || !it->second.live || it->second.bytes != ((size_t)CRC32C_PAGE_SIZE << order)) {
+		fprintf(stderr, "pech_crc32c: crc32c_pages_free(%p, %u): not a live allocation of that order\n", pages,
+			order);
+		abort(); // a bad free in pech is a BUG_ON (src/page.c keeps no checks)
+	}
+	if (order <= kMaxOrder && g_free[order].size() < (kMaxCachedPerOrder >> CRC32C_PAGE_SHIFT >> order)) {
+		it->second.live = false;
+		g_free[order].push_back(pages);
+		return;
+	}
+	g_pages.erase(it);
+	(void)hipHostFree(pages);
+}
+
+extern "C" int crc32c_pages_is_pinned(const void *p, size_t len)
+{
+	std::lock_guard<std::mutex> lk(g_pages_mu);
+	return find_live(p, len) != g_pages.end();
+}
+
+extern "C" void crc32c_pages_trim(void)
+{
+	std::lock_guard<std::mutex> lk(g_pages_mu);
+	for (auto &fl : g_free) {
+		for (void *p : fl) {
+			g_pages.erase((uintptr_t)p);
+			(void)hipHostFree(p);
+		}
+		fl.clear();
+	}
+}
+
+// device address of pinned host bytes p (inside a live allocation), or 0
+static uint64_t pinned_dev_addr(const void *p, size_t len)
+{
+	std::lock_guard<std::mutex> lk(g_pages_mu);
+	auto it = find_live(p, len);
+	if (it == g_pages.end())
+		return 0;
+	return (uint64_t)(uintptr_t)it->second.dev + ((uintptr_t)p - it->first);
+}
+
+// ===========================================================================
+// async contexts
+namespace {
+
+constexpr size_t kSlotBytes = 32u << 20; // staging per slot
+constexpr uint32_t kSlotDescs = 8192;    // descriptors per slot
+constexpr unsigned kMaxSlots = 4;        // slots in flight per context
+
+struct Piece {
+	uint64_t item; // submission id
+	uint32_t len;
+};
+
+struct Slot {
+	uint8_t *h_stage = nullptr, *d_stage = nullptr;
+	pech_desc *h_desc = nullptr, *d_desc = nullptr;
+	uint32_t *h_out = nullptr, *d_out = nullptr;
+	hipEvent_t done = nullptr;
+	std::vector<Piece> pieces;
+	std::vector<std::pair<size_t, size_t>> packed; // staging runs filled by memcpy: [lo, hi)
+	size_t used = 0;
+	bool inflight = false;
+};
+
+struct Item {
+	crc32c_done_fn done;
+	void *arg;
+	uint32_t crc;       // folded result of the harvested pieces
+	uint32_t harvested; // pieces whose results are folded in
+	uint32_t total;     // pieces placed (valid once `placed`)
+	bool placed;        // every piece has been given a descriptor
+	int err;
+};
+
+} // namespace
+
+struct crc32c_async {
+	int dev = -1;
+	unsigned flags = 0;
+	hipStream_t stream = nullptr;
+	int efd = -1;
+	void *d_ws = nullptr;
+	size_t ws_bytes = 0;
+	std::vector<Slot *> slots;
+	std::deque<Slot *> inflight; // launch order
+	Slot *cur = nullptr;         // slot being filled
+	std::deque<Item> items;      // items[k] is submission id base + k
+	uint64_t base = 0;
+	int err = 0;                 // sticky failure of this context
+};
+
+static void slot_free(Slot *s)
+{
+	if (s->h_stage)
+		(void)hipHostFree(s->h_stage);
+	if (s->d_stage)
+		(void)hipFree(s->d_stage);
+	if (s->h_desc)
+		(void)hipHostFree(s->h_desc);
+	if (s->d_desc)
+		(void)hipFree(s->d_desc);
+	if (s->h_out)
+		(void)hipHostFree(s->h_out);
+	if (s->d_out)
+		(void)hipFree(s->d_out);
+	if (s->done)
+		(void)hipEventDestroy(s->done);
+	delete s;
+}
+
+static Slot *slot_new(void)
+{
+	Slot *s = new Slot();
+	if (hipHostMalloc(&s->h_stage, kSlotBytes, hipHostMallocDefault) != hipSuccess ||
+	    hipMalloc(&s->d_stage, kSlotBytes) != hipSuccess ||
+	    hipHostMalloc(&s->h_desc, kSlotDescs * sizeof(pech_desc), hipHostMallocDefault) != hipSuccess ||
+	    hipMalloc(&s->d_desc, kSlotDescs * sizeof(pech_desc)) != hipSuccess ||
+	    hipHostMalloc(&s->h_out, kSlotDescs * 4u, hipHostMallocDefault) != hipSuccess ||
+	    hipMalloc(&s->d_out, kSlotDescs * 4u) != hipSuccess ||
+	    hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess) {
+		pech_internal_set_err("crc32c_async: slot allocation failed: %s", hipGetErrorString(hipGetLastError()));
+		slot_free(s);
+		return nullptr;
+	}
+	s->pieces.reserve(kSlotDescs);
+	return s;
+}
+
+static void host_notify(void *arg)
+{
+	// HIP runtime thread: only the eventfd is touched here
+	const uint64_t one = 1;
+	ssize_t r = write(*(int *)arg, &one, sizeof(one));
+	(void)r;
+}
+
+// fold a harvested slot's results into its items; slot becomes reusable
+static void harvest(crc32c_async *a, Slot *s, int err)
+{
+	for (size_t k = 0; k < s->pieces.size(); ++k) {
+		const Piece &pc = s->pieces[k];
+		Item &it = a->items[pc.item - a->base];
+		if (err)
+			it.err = err;
+		else
+			// pieces arrive in byte order (slots complete in launch order);
+			// piece 0 carried the seed, the rest were checksummed from 0
+			it.crc = it.harvested == 0 ? s->h_out[k] : crc32c_combine(it.crc, s->h_out[k], pc.len);
+		it.harvested++;
+	}
+	s->pieces.clear();
+	s->packed.clear();
+	s->used = 0;
+	s->inflight = false;
+}
+
+// Harvest finished slots (blocking on the oldest when `wait`), in order.
+static int reap(crc32c_async *a, bool wait_oldest)
+{
+	while (!a->inflight.empty()) {
+		Slot *s = a->inflight.front();
+		hipError_t q = wait_oldest ? hipEventSynchronize(s->done) : hipEventQuery(s->done);
+		if (q == hipErrorNotReady)
+			return 0;
+		int err = 0;
+		if (q != hipSuccess) {
+			pech_internal_set_err("crc32c_async: batch failed: %s", hipGetErrorString(q));
+			err = -EIO;
+			a->err = err;
+		}
+		a->inflight.pop_front();
+		harvest(a, s, err);
+		if (wait_oldest)
+			return err;
+	}
+	return 0;
+}
+
+static int get_slot(crc32c_async *a, Slot **out)
+{
+	if (a->cur) {
+		*out = a->cur;
+		return 0;
+	}
+	for (Slot *s : a->slots)
+		if (!s->inflight) {
+			a->cur = *out = s;
+			return 0;
+		}
+	if (a->slots.size() < kMaxSlots) {
+		Slot *s = slot_new();
+		if (!s)
+			return -ENOMEM;
+		a->slots.push_back(s);
+		a->cur = *out = s;
+		return 0;
+	}
+	// every slot in flight: wait for the oldest (callbacks still run only
+	// in crc32c_async_complete)
+	int rc = reap(a, true);
+	if (rc)
+		return rc;
+	return get_slot(a, out);
+}
+
+static int launch_slot(crc32c_async *a)
+{
+	Slot *s = a->cur;
+	if (!s || s->pieces.empty())
+		return 0;
+	const unsigned m = (unsigned)s->pieces.size();
+	for (auto &r : s->packed)
+		TRY_HIP(hipMemcpyAsync(s->d_stage + r.first, s->h_stage + r.first, r.second - r.first,
+				       hipMemcpyHostToDevice, a->stream),
+			-EIO);
+	TRY_HIP(hipMemcpyAsync(s->d_desc, s->h_desc, m * sizeof(pech_desc), hipMemcpyHostToDevice, a->stream), -EIO);
+	int rc = pech_internal_launch(s->d_desc, s->d_out, m, a->d_ws, a->ws_bytes, a->stream);
+	if (rc)
+		return rc;
+	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, a->stream), -EIO);
+	TRY_HIP(hipEventRecord(s->done, a->stream), -EIO);
+	TRY_HIP(hipLaunchHostFunc(a->stream, host_notify, &a->efd), -EIO);
+	s->inflight = true;
+	a->inflight.push_back(s);
+	a->cur = nullptr;
+	return 0;
+}
+
+extern "C" struct crc32c_async *crc32c_async_create(unsigned int flags)
+{
+	if (flags & ~CRC32C_ASYNC_ZEROCOPY) {
+		pech_internal_set_err("crc32c_async_create: unknown flags %#x", flags);
+		return nullptr;
+	}
+	if (crc32c_device_init())
+		return nullptr;
+	crc32c_async *a = new crc32c_async();
+	a->flags = flags;
+	a->ws_bytes = pech_ws_bytes(kSlotDescs);
+	if (hipGetDevice(&a->dev) != hipSuccess ||
+	    hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipMalloc(&a->d_ws, a->ws_bytes) != hipSuccess) {
+		pech_internal_set_err("crc32c_async_create: %s", hipGetErrorString(hipGetLastError()));
+		crc32c_async_destroy(a);
+		return nullptr;
+	}
+	a->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+	if (a->efd < 0) {
+		pech_internal_set_err("crc32c_async_create: eventfd: %s", strerror(errno));
+		crc32c_async_destroy(a);
+		return nullptr;
+	}
+	return a;
+}
+
+extern "C" int crc32c_async_fd(const struct crc32c_async *a)
+{
+	return a ? a->efd : -EINVAL;
+}
+
+extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsigned int len, uint32_t seed,
+				   crc32c_done_fn done, void *arg)
+{
+	if (!a || !done || (len && !buf)) {
+		pech_internal_set_err("crc32c_async_submit: invalid arguments");
+		return -EINVAL;
+	}
+	if (a->err)
+		return a->err;
+	const uint64_t id = a->base + a->items.size();
+	a->items.push_back(Item{done, arg, seed, 0u, 0u, false, 0});
+	const uint8_t *p = (const uint8_t *)buf;
+	size_t left = len;
+	uint32_t placed = 0;
+	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len ? pinned_dev_addr(buf, len) : 0;
+	const bool dma = !zc && len && crc32c_pages_is_pinned(buf, len);
+	do {
+		Slot *s = nullptr;
+		int rc = get_slot(a, &s);
+		if (rc)
+			return rc;
+		if (s->pieces.size() == kSlotDescs || (!zc && left && s->used >= kSlotBytes)) {
+			if ((rc = launch_slot(a)))
+				return rc;
+			continue;
+		}
+		pech_desc &d = s->h_desc[s->pieces.size()];
+		size_t piece;
+		if (zc) {
+			piece = left; // read in place: no staging space
+			d.addr = zc + (len - left);
+		} else {
+			piece = left < kSlotBytes - s->used ? left : kSlotBytes - s->used;
+			d.addr = (uint64_t)(uintptr_t)(s->d_stage + s->used);
+			if (piece && dma) {
+				TRY_HIP(hipMemcpyAsync(s->d_stage + s->used, p, piece, hipMemcpyHostToDevice, a->stream),
+					-EIO);
+			} else if (piece) {
+				memcpy(s->h_stage + s->used, p, piece);
+				if (!s->packed.empty() && s->packed.back().second == s->used)
+					s->packed.back().second = s->used + piece;
+				else
+					s->packed.push_back({s->used, s->used + piece});
+			}
+			s->used = (s->used + piece + 255u) & ~(size_t)255u;
+		}
+		d.len = (uint32_t)piece;
+		d.seed = placed == 0 ? seed : 0u;
+		s->pieces.push_back(Piece{id, (uint32_t)piece});
+		++placed;
+		p += piece;
+		left -= piece;
+	} while (left);
+	Item &it = a->items[id - a->base];
+	it.placed = true;
+	it.total = placed;
+	Slot *s = a->cur;
+	if (s && (s->pieces.size() == kSlotDescs || s->used >= kSlotBytes))
+		return launch_slot(a);
+	return 0;
+}
+
+extern "C" int crc32c_async_flush(struct crc32c_async *a)
+{
+	if (!a)
+		return -EINVAL;
+	if (a->err)
+		return a->err;
+	return launch_slot(a);
+}
+
+// items are finished when every placed piece has been harvested
+static int run_callbacks(crc32c_async *a)
+{
+	int ran = 0;
+	while (!a->items.empty()) {
+		Item &it = a->items.front();
+		if (!it.placed || it.harvested != it.total)
+			break;
+		const Item done = it;
+		a->items.pop_front();
+		a->base++;
+		done.done(done.arg, done.err ? 0u : done.crc, done.err);
+		++ran;
+	}
+	return ran;
+}
+
+extern "C" int crc32c_async_complete(struct crc32c_async *a)
+{
+	if (!a)
+		return -EINVAL;
+	uint64_t cnt;
+	while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
+	}
+	int rc = reap(a, false);
+	int ran = run_callbacks(a);
+	return rc ? rc : ran;
+}
+
+extern "C" int crc32c_async_drain(struct crc32c_async *a)
+{
+	if (!a)
+		return -EINVAL;
+	int rc = a->err ? a->err : launch_slot(a);
+	while (!a->inflight.empty()) {
+		int r = reap(a, true);
+		if (r && !rc)
+			rc = r;
+	}
+	uint64_t cnt;
+	while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
+	}
+	run_callbacks(a);
+	return rc;
+}
+
+extern "C" unsigned int crc32c_async_pending(const struct crc32c_async *a)
+{
+	return a ? (unsigned int)a->items.size() : 0u;
+}
+
+extern "C" void crc32c_async_destroy(struct crc32c_async *a)
+{
+	if (!a)
+		return;
+	if (a->stream) {
+		(void)crc32c_async_drain(a);
+		(void)hipStreamSynchronize(a->stream);
+	}
+	for (Slot *s : a->slots)
+		slot_free(s);
+	if (a->d_ws)
+		(void)hipFree(a->d_ws);
+	if (a->stream)
+		(void)hipStreamDestroy(a->stream);
+	if (a->efd >= 0)
+		close(a->efd);
+	delete a;
+}

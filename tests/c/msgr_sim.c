@@ -1,0 +1,169 @@
+/*
+ * msgr_sim.c -- TEST PROGRAM: pech's receive path on libpech_crc32c's async
+ * layer, in pech's own dialect (gnu89 C, one OS thread, epoll loop).
+ *
+ * What it plays out (file:line in /root/reference):
+ *   - osds_alloc_msg() -> alloc_bvec(): every message's data section is ONE
+ *     contiguous 2^order-page buffer (src/ceph/osd_server.c:2317-2381,
+ *     :208-215); here from crc32c_pages_alloc() (pinned) or, for every
+ *     third message, plain malloc (pageable), both paths of the library.
+ *   - read_partial_msg_data() (src/ceph/messenger.c:2649-2684): bytes arrive;
+ *     the reference chains crc32c() per <=4 KiB piece as they come.  Here the
+ *     payload is submitted ONCE when total_resid reaches 0.
+ *   - the footer check (messenger.c:2836-2842): the callback compares the
+ *     GPU result with footer.data_crc, which the sender computed with the
+ *     reference per-piece chain (oracle_crc32c_pieces, the test oracle).
+ *   - the event loop (src/event.c:52-70): epoll_wait on the context's
+ *     eventfd, as an event_item would (include/event.h:7-28).
+ * Exit status 0 iff every message verified and none is left pending.
+ *
+ * Build (tests/test_async.py does it):
+ *   gcc -std=gnu89 -O2 -Iinclude tests/c/msgr_sim.c oracle/crc32c_oracle.c \
+ *       -Lpech_amd -lpech_crc32c -Wl,-rpath,$PWD/pech_amd -o build/msgr_sim
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/epoll.h>
+
+#include "pech_crc32c_async.h"
+
+/* the test oracle (oracle/crc32c_oracle.c): reference loop, per-piece chain */
+uint32_t oracle_crc32c_pieces(uint32_t crc, const void *data, size_t length, unsigned int piece);
+
+struct msg {
+	unsigned char *data;
+	unsigned int data_len;
+	unsigned int order; /* pages order, or ~0u for malloc */
+	uint32_t footer_data_crc; /* what the peer put on the wire */
+	int verified;
+};
+
+static unsigned int nr_bad, nr_done;
+
+static void data_crc_done(void *arg, uint32_t crc, int err)
+{
+	struct msg *m = arg;
+
+	if (err || crc != m->footer_data_crc) {
+		fprintf(stderr, "bad crc: len %u got %08x want %08x err %d\n", m->data_len, crc, m->footer_data_crc,
+			err);
+		nr_bad++;
+	}
+	m->verified = 1;
+	nr_done++;
+}
+
+static unsigned int order_for(unsigned int len)
+{
+	unsigned int o = 0;
+
+	while ((CRC32C_PAGE_SIZE << o) < len)
+		o++;
+	return o;
+}
+
+static uint32_t xs = 0x2545F491u;
+
+static unsigned char next_byte(void)
+{
+	xs ^= xs << 13;
+	xs ^= xs >> 17;
+	xs ^= xs << 5;
+	return (unsigned char)xs;
+}
+
+int main(int argc, char **argv)
+{
+	static const unsigned int sizes[] = {0, 1, 100, 4096, 4097, 65536, 131072, 1 << 20, (4 << 20) + 3,
+					     (40 << 20) + 17};
+	unsigned int nmsgs = argc > 1 ? (unsigned int)atoi(argv[1]) : 300;
+	unsigned int zerocopy = argc > 2 ? (unsigned int)atoi(argv[2]) : 0;
+	struct crc32c_async *a;
+	struct epoll_event ev, out;
+	struct msg *msgs;
+	unsigned int i, k;
+	int ep, rc;
+
+	a = crc32c_async_create(zerocopy ? CRC32C_ASYNC_ZEROCOPY : CRC32C_ASYNC_DEFAULT);
+	if (!a) {
+		fprintf(stderr, "crc32c_async_create: %s\n", crc32c_last_error());
+		return 2;
+	}
+	ep = epoll_create1(0);
+	memset(&ev, 0, sizeof(ev));
+	ev.events = EPOLLIN;
+	ev.data.fd = crc32c_async_fd(a);
+	if (ep < 0 || epoll_ctl(ep, EPOLL_CTL_ADD, ev.data.fd, &ev)) {
+		perror("epoll");
+		return 2;
+	}
+	msgs = calloc(nmsgs, sizeof(*msgs));
+	for (i = 0; i < nmsgs; i++) {
+		struct msg *m = &msgs[i];
+
+		m->data_len = sizes[(i * 7u) % (sizeof(sizes) / sizeof(sizes[0]))];
+		if (i % 3 == 2) {
+			m->order = ~0u;
+			m->data = malloc(m->data_len ? m->data_len : 1);
+		} else {
+			m->order = order_for(m->data_len);
+			m->data = crc32c_pages_alloc(m->order);
+		}
+		if (!m->data) {
+			fprintf(stderr, "alloc: %s\n", crc32c_last_error());
+			return 2;
+		}
+		/* "receive" the payload, then the peer's footer */
+		for (k = 0; k < m->data_len; k++)
+			m->data[k] = next_byte();
+		m->footer_data_crc = oracle_crc32c_pieces(0, m->data, m->data_len, 4096);
+		/* total_resid == 0: one submission for the whole payload */
+		rc = crc32c_async_submit(a, m->data, m->data_len, 0, data_crc_done, m);
+		if (rc) {
+			fprintf(stderr, "submit: %d %s\n", rc, crc32c_last_error());
+			return 2;
+		}
+		/* the connection's read burst ends every 16 messages: flush */
+		if (i % 16 == 15 && (rc = crc32c_async_flush(a))) {
+			fprintf(stderr, "flush: %d %s\n", rc, crc32c_last_error());
+			return 2;
+		}
+		/* opportunistic completions between reads, without blocking */
+		if (i % 5 == 0 && crc32c_async_complete(a) < 0)
+			return 2;
+	}
+	if ((rc = crc32c_async_flush(a))) {
+		fprintf(stderr, "flush: %d %s\n", rc, crc32c_last_error());
+		return 2;
+	}
+	/* the event loop: wait for the eventfd, complete, until nothing pending */
+	while (crc32c_async_pending(a)) {
+		int n = epoll_wait(ep, &out, 1, 10000);
+
+		if (n < 0) {
+			perror("epoll_wait");
+			return 2;
+		}
+		if (n == 0) {
+			fprintf(stderr, "timeout: %u pending\n", crc32c_async_pending(a));
+			return 3;
+		}
+		if (crc32c_async_complete(a) < 0) {
+			fprintf(stderr, "complete: %s\n", crc32c_last_error());
+			return 2;
+		}
+	}
+	for (i = 0; i < nmsgs; i++) {
+		if (!msgs[i].verified)
+			nr_bad++;
+		if (msgs[i].order == ~0u)
+			free(msgs[i].data);
+		else
+			crc32c_pages_free(msgs[i].data, msgs[i].order);
+	}
+	crc32c_async_destroy(a);
+	crc32c_pages_trim();
+	printf("msgr_sim: %u messages, %u verified, %u bad (zerocopy %u)\n", nmsgs, nr_done, nr_bad, zerocopy);
+	return nr_bad ? 1 : 0;
+}
