@@ -49,13 +49,16 @@ struct crc32c_desc {
 /* flags for crc32c_batch() */
 #define CRC32C_F_HOST 0u   /* bufs are pageable host memory                */
 #define CRC32C_F_DEVICE 1u /* bufs are device memory on the current device */
-#define CRC32C_F_PINNED 2u /* bufs are pinned host memory (DMA directly)   */
+#define CRC32C_F_PINNED 2u /* bufs are pinned host memory (read in place)   */
 
 /*
  * out[i] = crc32c(seeds ? seeds[i] : 0, bufs[i], lens[i]) for i < n.
- * Synchronous.  Host buffers are moved with hipMemcpyAsync through pinned
- * staging (double-buffered, overlapped with the kernel); results come back
- * with one D2H copy per sub-batch.
+ * Synchronous.  Pageable host buffers are moved with hipMemcpyAsync through
+ * pinned staging (double-buffered, overlapped with the kernel); pinned
+ * buffers (CRC32C_F_PINNED: hipHostMalloc'd or registered) are read by the
+ * kernel in place through their device mapping (zero-copy), falling back to
+ * DMA staging if a buffer has none.  Results come back with one D2H copy per
+ * sub-batch.
  */
 int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
 		 uint32_t *out, unsigned int n, unsigned int flags);

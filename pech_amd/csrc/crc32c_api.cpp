@@ -347,10 +347,50 @@ static int host_big(DevCtx *c, const void *buf, size_t len, uint32_t seed, uint3
 	return 0;
 }
 
+// Pinned host buffers read in place by the kernel over the host link
+// (zero-copy: hipHostMalloc'd / registered memory is mapped into the GPU's
+// address space).  Measured faster than DMA staging on MI355X boxes (bench
+// msgr_async).  Returns 1 if some buffer has no device mapping (caller
+// falls back to DMA staging).
+static int pinned_zero_copy(DevCtx *c, const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
+			    uint32_t *out, unsigned int n)
+{
+	int rc = stage_reserve(c, c->stage_bytes ? c->stage_bytes : STAGE_BYTES, STAGE_DESCS);
+	if (rc)
+		return rc;
+	for (unsigned int i0 = 0; i0 < n; i0 += STAGE_DESCS) {
+		const unsigned int m = (n - i0) < STAGE_DESCS ? (n - i0) : STAGE_DESCS;
+		for (unsigned int k = 0; k < m; ++k) {
+			void *dp = nullptr;
+			const unsigned int i = i0 + k;
+			if (lens[i] && (hipHostGetDevicePointer(&dp, const_cast<void *>(bufs[i]), 0) != hipSuccess || !dp)) {
+				(void)hipGetLastError();
+				return i0 == 0 ? 1 : -EIO; // nothing launched yet: fall back
+			}
+			c->h_desc[0][k].addr = (uint64_t)(uintptr_t)dp;
+			c->h_desc[0][k].len = lens[i];
+			c->h_desc[0][k].seed = seeds ? seeds[i] : 0u;
+		}
+		HIP_TRY(hipMemcpyAsync(c->d_desc[0], c->h_desc[0], (size_t)m * sizeof(pech_desc), hipMemcpyHostToDevice,
+				       c->s_comp));
+		if ((rc = ws_reserve(c, m)))
+			return rc;
+		if ((rc = launch_batch(c, c->d_desc[0], c->d_out[0], m, c->d_ws, c->ws_bytes, c->s_comp)))
+			return rc;
+		HIP_TRY(hipMemcpyAsync(c->h_out[0], c->d_out[0], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
+		HIP_TRY(hipStreamSynchronize(c->s_comp));
+		memcpy(out + i0, c->h_out[0], (size_t)m * 4u);
+	}
+	return 0;
+}
+
 static int host_batch(DevCtx *c, const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
 		      uint32_t *out, unsigned int n, unsigned int flags)
 {
-	int rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
+	int rc;
+	if ((flags & CRC32C_F_PINNED) && (rc = pinned_zero_copy(c, bufs, lens, seeds, out, n)) <= 0)
+		return rc;
+	rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
 	if (rc)
 		return rc;
 	// slot bookkeeping for the double buffer
