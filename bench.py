@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive pinned-host leg")
     ap.add_argument("--host-passes", type=int, default=4)
+    ap.add_argument("--op", default="crc", choices=["crc", "copy"],
+                    help="crc: the checksum path; copy: fused CRC + copy to a second buffer (SURVEY 8f row 4)")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams that consecutive batches alternate over (own workspace each)")
     ap.add_argument("--pipeline-streams", type=int, default=2,
@@ -115,6 +117,11 @@ def main():
         bufs.append(b)
         descs.append(P.make_descs(b.data_ptr() + offs, sizes, device=dev))
     outs = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(rotate)]
+    dsts = []
+    if args.op == "copy":  # a destination buffer per rotating batch, same layout
+        for r in range(rotate):
+            d = torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
+            dsts.append((d, torch.from_numpy((d.data_ptr() + offs).astype(np.int64)).to(dev)))
     assert _lib.lib().crc32c_dev_reserve(n) == 0
     maxs = max(1, args.streams, args.pipeline_streams)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(maxs - 1)]
@@ -131,7 +138,11 @@ def main():
 
         def step(i):
             k = i % nstreams
-            P.dev_batch_ws_async(descs[i % rotate], outs[i % rotate], wss[k], stream=streams[k])
+            if dsts:
+                P.dev_copy_batch_ws_async(descs[i % rotate], dsts[i % rotate][1], outs[i % rotate], wss[k],
+                                          stream=streams[k])
+            else:
+                P.dev_batch_ws_async(descs[i % rotate], outs[i % rotate], wss[k], stream=streams[k])
 
         for i in range(warmup):
             step(i)
@@ -165,13 +176,17 @@ def main():
     total_bytes = batch_bytes * args.steps * world
     value = total_bytes / elapsed / (1 << 30)
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
-    achieved_gbs = batch_bytes / avg_kernel_s / 1e9 if launches else 0.0
+    # algorithmic HBM bytes per launch: each payload byte read once (+ written
+    # once by the fused copy)
+    algo_bytes = batch_bytes * (2 if dsts else 1)
+    achieved_gbs = algo_bytes / avg_kernel_s / 1e9 if launches else 0.0
 
     # HBM bytes per launch from the committed rocprofv3 PMC pass of this
     # config (tools/pmc_traffic.py: FETCH_SIZE x 2, the gfx950 correction of
     # MI355X_MICROARCH.md), used only when it was taken on this kernel build.
     traffic = None
-    pj = args.profile_json or os.path.join(REPO, "profiles", "r01", f"{args.config}_traffic.json")
+    tag = args.config + ("-copy" if dsts else "")
+    pj = args.profile_json or os.path.join(REPO, "profiles", "r01", f"{tag}_traffic.json")
     if os.path.exists(pj):
         prof = json.load(open(pj))
         if prof.get("kernel") == P.version():
@@ -190,13 +205,15 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (uniform random bytes, torch.randint on device), seed 0 per buffer",
-        "config": {"workload": desc, "buffers_per_gpu": n, "bytes_per_gpu_per_step": batch_bytes,
+        "config": {"workload": desc + ("; fused CRC + copy to a second buffer (read + write)" if dsts else ""),
+                   "buffers_per_gpu": n, "bytes_per_gpu_per_step": batch_bytes,
                    "parallelism": f"shard{world} (independent buffers per GPU, no collective)",
                    "streams": nstreams,
                    "kernel": P.version()},
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "pech_crc32c_main", "avg_launch_us": round(avg_kernel_s * 1e6, 2),
+                     "kernel": "pech_crc32c_main_copy" if dsts else "pech_crc32c_main",
+                     "bytes_per_launch": algo_bytes, "avg_launch_us": round(avg_kernel_s * 1e6, 2),
                      "launch_us_p10_p50_p90": [round(float(np.percentile(samples, q)), 2) for q in (10, 50, 90)]
                      if len(samples) else None,
                      "launches": launches},
@@ -212,12 +229,12 @@ def main():
                              "value": round(total_bytes / pel / (1 << 30), 2), "unit": "GiB/s",
                              "ms_per_step": round(pel / args.steps * 1e3, 4),
                              "avg_launch_us": round(float(psamp.mean()), 2) if len(psamp) else None}
-    if rank == 0 and world == 1 and not args.no_host_path:
+    if rank == 0 and world == 1 and not args.no_host_path and not dsts:
         line["pcie_inclusive"] = host_path(args, bufs[0], offs, sizes, outs, P)
         # per-payload submits go through ctypes here: only measured where the
         # payloads are large enough for the Python loop not to be the bound
         line["msgr_async"] = msgr_path(args, bufs[0], offs, sizes, outs, P) if n <= 4096 else None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not dsts:
         line["cpu_baseline"] = cpu_baseline(args, bufs[0], offs, sizes, outs, rotate, P)
 
     if rank == 0:

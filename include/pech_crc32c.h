@@ -14,6 +14,8 @@
  *                            piece (bit-identical by the chaining law).
  *   crc32c_dev_batch_*    -- same, over device-resident buffers (GPU-resident
  *                            object data; no reference counterpart).
+ *   crc32c_dev_copy_batch_* -- CRC fused with the copy memstore makes of the
+ *                            same bytes (src/ceph/memstore.c:306, :445).
  *   crc32c_combine/_shift -- CRC reuse across replica sends
  *                            (src/ceph/osd_server.c:1119 nested cursor,
  *                            :1972 per-replica ceph_con_send) and page-piece
@@ -81,6 +83,22 @@ int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, u
 size_t crc32c_dev_workspace_bytes(unsigned int n);
 int crc32c_dev_batch_ws_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n,
 			      void *d_workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * Fused CRC + copy, device batch, asynchronous on `stream`:
+ *   d_out[i] = crc32c(d_descs[i].seed, d_descs[i].addr, d_descs[i].len)  and
+ *   the len bytes at d_descs[i].addr are copied to d_dsts[i]
+ * in ONE pass over the source bytes (each read once from HBM, written once).
+ * Replaces the CRC pass plus the separate gathers of memstore's write path
+ * (copy_from_iter into 64 KiB blocks, src/ceph/memstore.c:306) and read path
+ * (memcpy gather, :445).  Any source / destination alignment; destination
+ * ranges must not overlap any source range of the batch (as for memcpy).
+ * Same workspace rules as crc32c_dev_batch_*.
+ */
+int crc32c_dev_copy_batch_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
+				unsigned int n, void *stream);
+int crc32c_dev_copy_batch_ws_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
+				   unsigned int n, void *d_workspace, size_t workspace_bytes, void *stream);
 
 /* Pre-size the internal workspace of the current device for n buffers. */
 int crc32c_dev_reserve(unsigned int n);

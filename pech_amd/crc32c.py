@@ -15,7 +15,7 @@ from ._lib import CDesc, Crc32cError, check, lib
 
 __all__ = [
     "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
-    "dev_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
+    "dev_batch_ws_async", "dev_copy_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
     "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc",
 ]
 
@@ -112,6 +112,20 @@ def dev_batch_ws_async(descs, out, ws, stream=None):
         stream = torch.cuda.current_stream(descs.device)
     check(lib().crc32c_dev_batch_ws_async(descs.data_ptr(), out.data_ptr(), n, ws.data_ptr(), ws.numel(),
                                           stream.cuda_stream), "crc32c_dev_batch_ws_async")
+
+
+def dev_copy_batch_ws_async(descs, dsts, out, ws, stream=None):
+    """Fused CRC + copy (crc32c_dev_copy_batch_ws_async): dsts is an (n,)
+    int64 device tensor of destination addresses."""
+    import torch
+
+    n = descs.shape[0]
+    if out.numel() < n or out.element_size() != 4 or dsts.numel() < n or dsts.element_size() != 8:
+        raise ValueError("out must hold n 32-bit words, dsts n 64-bit addresses")
+    if stream is None:
+        stream = torch.cuda.current_stream(descs.device)
+    check(lib().crc32c_dev_copy_batch_ws_async(descs.data_ptr(), dsts.data_ptr(), out.data_ptr(), n, ws.data_ptr(),
+                                               ws.numel(), stream.cuda_stream), "crc32c_dev_copy_batch_ws_async")
 
 
 def crc32c_tensors(tensors, seeds=None, offsets=None, lengths=None):

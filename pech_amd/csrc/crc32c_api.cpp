@@ -23,8 +23,8 @@ static_assert(sizeof(struct crc32c_desc) == sizeof(struct pech_desc), "descripto
 static_assert(sizeof(struct crc32c_desc) == 16, "descriptor ABI");
 
 extern "C" hipError_t pech_launch_plan(const pech_desc *, uint32_t, const pech_ws *, const uint32_t *, uint32_t *,
-				       hipStream_t);
-extern "C" hipError_t pech_launch_main(uint32_t, const pech_ws *, const uint32_t *, uint32_t *, uint32_t, uint32_t,
+				       const uint64_t *, hipStream_t);
+extern "C" hipError_t pech_launch_main(uint32_t, const pech_ws *, const uint32_t *, uint32_t *, uint32_t, uint32_t, int,
 				       hipStream_t, hipEvent_t, hipEvent_t);
 
 extern "C" const char *pech_kernel_tag(void);
@@ -171,8 +171,9 @@ static int ws_reserve(DevCtx *c, unsigned int n)
 	return 0;
 }
 
+// d_dsts != NULL: fused CRC + copy (d_dsts[i] receives descriptor i's bytes)
 static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-			size_t ws_bytes, hipStream_t stream)
+			size_t ws_bytes, hipStream_t stream, const uint64_t *d_dsts = nullptr)
 {
 	if (n == 0)
 		return 0;
@@ -187,7 +188,8 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			return -EINVAL;
 		}
 		const pech_ws w = pech_ws_carve(ws, m);
-		HIP_TRY(pech_launch_plan(d_descs + off, m, &w, c->d_consts, d_out + off, stream));
+		HIP_TRY(pech_launch_plan(d_descs + off, m, &w, c->d_consts, d_out + off, d_dsts ? d_dsts + off : nullptr,
+					 stream));
 		TimedLaunch tl{};
 		if (g_timing) {
 			if (!c->free_events.empty()) {
@@ -198,8 +200,8 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 				HIP_TRY(hipEventCreate(&tl.b));
 			}
 		}
-		HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN, stream, tl.a,
-					 tl.b));
+		HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN, d_dsts != nullptr,
+					 stream, tl.a, tl.b));
 		if (g_timing)
 			c->pending.push_back(tl);
 	}
@@ -565,6 +567,42 @@ int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, u
 	if ((rc = ws_reserve(c, n)))
 		return rc;
 	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, c->d_ws, c->ws_bytes, (hipStream_t)stream);
+}
+
+int crc32c_dev_copy_batch_ws_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
+				   unsigned int n, void *d_ws, size_t ws_bytes, void *stream)
+{
+	if (n == 0)
+		return 0;
+	if (!d_descs || !d_dsts || !d_out || !d_ws) {
+		set_err("crc32c_dev_copy_batch_ws_async: invalid arguments");
+		return -EINVAL;
+	}
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (rc)
+		return rc;
+	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, d_ws, ws_bytes, (hipStream_t)stream, d_dsts);
+}
+
+int crc32c_dev_copy_batch_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
+				unsigned int n, void *stream)
+{
+	if (n == 0)
+		return 0;
+	if (!d_descs || !d_dsts || !d_out) {
+		set_err("crc32c_dev_copy_batch_async: invalid arguments");
+		return -EINVAL;
+	}
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (rc)
+		return rc;
+	if ((rc = ws_reserve(c, n)))
+		return rc;
+	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, c->d_ws, c->ws_bytes, (hipStream_t)stream, d_dsts);
 }
 
 uint32_t crc32c_shift(uint32_t v, uint64_t nbytes)

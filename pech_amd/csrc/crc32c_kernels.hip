@@ -36,6 +36,9 @@
 #ifndef PECH_U
 #define PECH_U 8 // rows in flight per lane
 #endif
+#ifndef PECH_U_COPY
+#define PECH_U_COPY 8 // rows in flight per lane, fused-copy variant
+#endif
 #ifndef PECH_MAIN_WAVES
 #define PECH_MAIN_WAVES 16 // waves per main-kernel workgroup (one workgroup per CU)
 #endif
@@ -170,10 +173,25 @@ __device__ __forceinline__ uint32_t crc_bytes(const uint32_t *t1, uint32_t crc, 
 	return crc;
 }
 
-extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
-	const pech_desc *__restrict__ descs, uint32_t n, pech_core *__restrict__ cores, uint32_t *__restrict__ lrs,
-	uint32_t *__restrict__ partials, uint32_t *__restrict__ nzs, const uint32_t *__restrict__ consts,
-	uint32_t *__restrict__ out)
+// byte copy of [src, src + n) to src + dl (fused-copy variant: heads, tails
+// and buffers without a full aligned piece)
+__device__ __forceinline__ void copy_bytes(uint64_t src, int64_t dl, uint32_t n)
+{
+	const g_u8 *q = (const g_u8 *)src;
+	__attribute__((address_space(1))) uint8_t *d = (__attribute__((address_space(1))) uint8_t *)(src + dl);
+	for (uint32_t i = 0; i < n; ++i)
+		d[i] = q[i];
+}
+
+// COPY: also dst[b] <- bytes of buffer b (fused CRC + copy); the plan kernel
+// records dl = dst - src per buffer for the main kernel and copies the
+// bytes the main kernel does not (head, tail, or the whole tiny buffer).
+template <bool COPY>
+__device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, uint32_t n, pech_core *__restrict__ cores,
+					  uint32_t *__restrict__ lrs, uint32_t *__restrict__ partials,
+					  uint32_t *__restrict__ nzs, const uint32_t *__restrict__ consts,
+					  uint32_t *__restrict__ out, const uint64_t *__restrict__ dsts,
+					  int64_t *__restrict__ deltas)
 {
 	__shared__ uint32_t t1[256];
 	__shared__ uint32_t powb[384];
@@ -198,13 +216,24 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 		const uint64_t end = d.addr + d.len;
 		rows = pech_core_rows(d.addr, d.len);
 		uint32_t res;
+		int64_t dl = 0;
+		if (COPY) {
+			dl = (int64_t)(dsts[b] - d.addr);
+			deltas[b] = dl;
+		}
 		if (rows == 0) {
 			// no full aligned piece: the whole buffer here (<= 30 bytes)
 			res = crc_bytes(t1, d.seed, d.addr, d.len);
+			if (COPY)
+				copy_bytes(d.addr, dl, d.len);
 		} else {
 			const uint64_t cs = (d.addr + 15) & ~(uint64_t)15;
 			const uint64_t ce = end & ~(uint64_t)15;
 			const uint32_t h = (uint32_t)(cs - d.addr), t = (uint32_t)(end - ce);
+			if (COPY) {
+				copy_bytes(d.addr, dl, h);
+				copy_bytes(ce, dl, t);
+			}
 			res = 0;
 			if (d.seed)
 				res ^= shift_bytes(powb, d.len, d.seed);
@@ -244,6 +273,22 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
 		partials[blockIdx.x] = total;
 }
 
+extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
+	const pech_desc *__restrict__ descs, uint32_t n, pech_core *__restrict__ cores, uint32_t *__restrict__ lrs,
+	uint32_t *__restrict__ partials, uint32_t *__restrict__ nzs, const uint32_t *__restrict__ consts,
+	uint32_t *__restrict__ out)
+{
+	plan_body<false>(descs, n, cores, lrs, partials, nzs, consts, out, nullptr, nullptr);
+}
+
+extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan_copy(
+	const pech_desc *__restrict__ descs, uint32_t n, pech_core *__restrict__ cores, uint32_t *__restrict__ lrs,
+	uint32_t *__restrict__ partials, uint32_t *__restrict__ nzs, const uint32_t *__restrict__ consts,
+	uint32_t *__restrict__ out, const uint64_t *__restrict__ dsts, int64_t *__restrict__ deltas)
+{
+	plan_body<true>(descs, n, cores, lrs, partials, nzs, consts, out, dsts, deltas);
+}
+
 // ---- main kernel ----------------------------------------------------------
 #ifdef PECH_STAMPS // diagnostic build: per-wave entry/start/end s_memrealtime stamps
 #define PECH_MAX_STAMPS 8192u
@@ -273,6 +318,7 @@ struct Step {
 	uint32_t oz;  // orig | (zoff / 16) << 20               (zoff <= 112)
 	uint32_t T, nmin;
 	uint32_t pos, lr, rem;
+	uint64_t dad; // fused copy: destination of this lane's piece in row 0 (ad + dst - src)
 #ifdef PECH_DEBUG_BOUNDS
 	uint64_t blo, bhi; // core of the buffer this lane loads from
 #endif
@@ -372,11 +418,15 @@ __device__ __forceinline__ uint32_t slot_cw(uint32_t k)
 	return c;
 }
 
-// Work out the wave's next step from its cursor (pos, lr, rem).
-__device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const uint32_t *lds, uint32_t pos,
-					  uint32_t lr, uint32_t rem, uint32_t lane, uint32_t g8, uint32_t grp)
+// Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
+// the destination offset of each group's buffer (deltas[orig], scalar loads).
+template <bool COPY>
+__device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
+					  const uint32_t *lds, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
+					  uint32_t g8, uint32_t grp)
 {
 	Step S;
+	int64_t dl = 0;
 	S.T = 0;
 	S.nmin = 0;
 	S.ad = 0;
@@ -415,6 +465,8 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			S.mp = ((rows0 - st - nn) << 4) | PECH_META_TAIL(meta0);
 			S.T = q + (rm ? 1u : 0u);
 			S.nmin = q;
+			if (COPY)
+				dl = deltas[PECH_META_ORIG(meta0)];
 #ifdef PECH_DEBUG_BOUNDS
 			S.blo = vb0 + 16u * vp0;
 			S.bhi = vb0 + (uint64_t)rows0 * PECH_ROW_BYTES;
@@ -433,6 +485,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			// pos+7 may run past the chunk (or the cores array into lrs, still
 			// workspace memory); such entries are never used.
 			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
+			int64_t mdl = 0;
 #pragma unroll
 			for (uint32_t j = 0; j < 8; ++j) {
 				const pech_core dj = cores[pos + j];
@@ -441,6 +494,13 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 				vhi = mine ? uni((uint32_t)(dj.vbase >> 32)) : vhi;
 				mrows = mine ? uni(dj.rows) : mrows;
 				mmeta = mine ? uni(dj.meta) : mmeta;
+				if (COPY) {
+					// entries past the chunk are garbage: never index with them
+					const uint32_t pj = pos + j;
+					const bool okj = (pj & 1023u) < nzc && (pj >> 10) == c;
+					const int64_t dj_dl = deltas[okj ? PECH_META_ORIG(uni(dj.meta)) : 0u];
+					mdl = mine ? dj_dl : mdl;
+				}
 			}
 			pech_core my;
 			my.vbase = ((uint64_t)vhi << 32) | vlo;
@@ -490,6 +550,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 				zp = (lr == 0 && g8 < vp0) ? vp0 - g8 : 0u;
 			}
 			S.nu = nu;
+			dl = mdl;
 			S.oz = PECH_META_ORIG(my.meta) | (zp << 20);
 			S.mp = ((myrows - mylr - nu) << 4) | PECH_META_TAIL(my.meta);
 #ifdef PECH_DEBUG_BOUNDS
@@ -508,6 +569,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 	S.pos = pos;
 	S.lr = lr;
 	S.rem = rem;
+	S.dad = S.ad + (uint64_t)dl;
 	return S;
 }
 
@@ -524,7 +586,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 #define RING_PRIME(S, ring)                                                                           \
 	do {                                                                                          \
 		const uint32_t last_ = (S).nl - 1u;                                                   \
-		_Pragma("unroll") for (uint32_t i = 0; i + 1 < PECH_U; ++i) (ring)[i] =               \
+		_Pragma("unroll") for (uint32_t i = 0; i + 1 < U; ++i) (ring)[i] =                    \
 			LD_PIECE((S), row_addr((S).ad, min(i, last_), STEP_ZOFF(S)), 1);                 \
 	} while (0)
 
@@ -580,12 +642,24 @@ __device__ __forceinline__ void finish_run(const uint32_t *lds, uint32_t g8, uin
 	}
 }
 
-extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_main(
-	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
-	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min)
+// Fused copy: the consumed piece of row `row` of the lane's run goes to its
+// destination (S.dad: source + dst - src).  Virtual pieces (row 0 with zoff) and rows past
+// nu (clamped prefetch, idle groups) are never stored.
+template <bool COPY>
+__device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, bool ok)
 {
-	constexpr uint32_t U = PECH_U;
-	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
+	typedef __attribute__((address_space(1))) u32x4 g_u32x4w;
+	if (COPY && ok)
+		__builtin_nontemporal_store(v, (g_u32x4w *)(S.dad + (uint64_t)row * PECH_ROW_BYTES));
+}
+
+template <bool COPY, uint32_t U>
+__device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
+					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
+					  const uint32_t *__restrict__ nzs, uint32_t nchunks,
+					  const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min,
+					  const int64_t *__restrict__ deltas)
+{
 	const uint32_t tid = threadIdx.x;
 	STAMP(t_entry);
 
@@ -674,7 +748,7 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 		lr0 = uni(lr);
 	}
 	STAMP(t_find);
-	Step S = plan_step(cores, lds, p0, lr0, rem_all, lane, g8, grp);
+	Step S = plan_step<COPY>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp);
 	STAMP(t_plan);
 	if (S.T)
 		RING_PRIME(S, ring);
@@ -703,6 +777,7 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
 				horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
+				st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_ZOFF(S)));
 			}
 		}
 		// ragged blocks: clamped prefetch, predicated update
@@ -713,25 +788,28 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 				ring[(i + U - 1) % U] =
 					LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
 				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
+				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)));
 			}
 		}
 		// last block: its first load is this step's last row, the rest
 		// already fetch the next step's first rows
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
-		const Step N = plan_step(cores, lds, S.pos, S.lr, S.rem, lane, g8, grp);
+		const Step N = plan_step<COPY>(cores, deltas, lds, S.pos, S.lr, S.rem, lane, g8, grp);
 		horner_row_pred(lds, lreg, ring[0], r < S.nu, s0, s1, s2, s3);
-		if (N.T) {
-			const uint32_t nlast = N.nl - 1u;
+		st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_ZOFF(S)));
+		// Branch-free on purpose: with no next step the prefetch re-reads
+		// this step's last row (valid memory, never used).  An if/else here
+		// let LLVM sink the shared Horner code into a join block, which
+		// cost ring-register copies behind a vmcnt(0) at every step end.
+		const bool more = N.T != 0;
+		const Step &L = more ? N : S;
+		const uint32_t lrow0 = more ? 0u : last, lmax = more ? N.nl - 1u : last;
 #pragma unroll
-			for (uint32_t i = 1; i < U; ++i) {
-				ring[i - 1] = LD_PIECE(N, row_addr(N.ad, min(i - 1, nlast), STEP_ZOFF(N)), 5);
-				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
-			}
-		} else {
-#pragma unroll
-			for (uint32_t i = 1; i < U; ++i)
-				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
+		for (uint32_t i = 1; i < U; ++i) {
+			ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
+			horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
+			st_piece<COPY>(S, r + i, ring[i], r + i < S.nu);
 		}
 		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));
 		S = N;
@@ -754,13 +832,38 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 #endif
 }
 
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_main(
+	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
+	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	uint32_t rpw_min)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
+	main_body<false, PECH_U>(lds, cores, lrs, partials, nzs, nchunks, consts, out, rpw_min, nullptr);
+}
+
+// fused CRC + copy (include/pech_crc32c.h crc32c_dev_copy_batch_*): the same
+// walk, every consumed 16-byte piece also stored to its destination
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_main_copy(
+	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
+	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	uint32_t rpw_min, const int64_t *__restrict__ deltas)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
+	main_body<true, PECH_U_COPY>(lds, cores, lrs, partials, nzs, nchunks, consts, out, rpw_min, deltas);
+}
+
 // ---- host-side launchers (used by crc32c_api.cpp) -------------------------
+// dsts != NULL: the fused-copy variant (destination address per descriptor)
 extern "C" hipError_t pech_launch_plan(const pech_desc *descs, uint32_t n, const pech_ws *ws, const uint32_t *consts,
-				       uint32_t *out, hipStream_t stream)
+				       uint32_t *out, const uint64_t *dsts, hipStream_t stream)
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
-	hipLaunchKernelGGL(pech_crc32c_plan, dim3(nch), dim3(PECH_WG_THREADS), 0, stream, descs, n, ws->cores, ws->lrs,
-			   ws->partials, ws->nzs, consts, out);
+	if (dsts)
+		hipLaunchKernelGGL(pech_crc32c_plan_copy, dim3(nch), dim3(PECH_WG_THREADS), 0, stream, descs, n, ws->cores,
+				   ws->lrs, ws->partials, ws->nzs, consts, out, dsts, ws->deltas);
+	else
+		hipLaunchKernelGGL(pech_crc32c_plan, dim3(nch), dim3(PECH_WG_THREADS), 0, stream, descs, n, ws->cores,
+				   ws->lrs, ws->partials, ws->nzs, consts, out);
 	return hipGetLastError();
 }
 
@@ -768,13 +871,19 @@ extern "C" hipError_t pech_launch_plan(const pech_desc *descs, uint32_t n, const
 // (hipExtLaunchKernel), so their interval is the kernel's execution alone,
 // as rocprofv3's kernel trace reports it -- no launch boundary included.
 extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint32_t *consts, uint32_t *out,
-				       uint32_t ncu, uint32_t rpw_min, hipStream_t stream, hipEvent_t ev_start,
+				       uint32_t ncu, uint32_t rpw_min, int copy, hipStream_t stream, hipEvent_t ev_start,
 				       hipEvent_t ev_stop)
 {
 	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
-	hipExtLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u,
-			      (const pech_core *)ws->cores, (const uint32_t *)ws->lrs, (const uint32_t *)ws->partials,
-			      (const uint32_t *)ws->nzs, nch, consts, out, rpw_min);
+	if (copy)
+		hipExtLaunchKernelGGL(pech_crc32c_main_copy, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop,
+				      0u, (const pech_core *)ws->cores, (const uint32_t *)ws->lrs,
+				      (const uint32_t *)ws->partials, (const uint32_t *)ws->nzs, nch, consts, out, rpw_min,
+				      (const int64_t *)ws->deltas);
+	else
+		hipExtLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop,
+				      0u, (const pech_core *)ws->cores, (const uint32_t *)ws->lrs,
+				      (const uint32_t *)ws->partials, (const uint32_t *)ws->nzs, nch, consts, out, rpw_min);
 	return hipGetLastError();
 }
 
@@ -782,6 +891,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.6 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.7 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }

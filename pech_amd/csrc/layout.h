@@ -101,10 +101,12 @@ LAYOUT_FN uint32_t pech_size_class(uint32_t rows)
  *   lrs      u32[slots]              chunk-local exclusive row scan
  *   partials u32[PECH_MAX_CHUNKS]    rows per chunk
  *   nzs      u32[PECH_MAX_CHUNKS]    non-empty cores per chunk
+ *   deltas   i64[slots]              fused copy: destination - source per buffer
  * slots = nch * PECH_CHUNK, nch = ceil(m / PECH_CHUNK). */
 struct pech_ws {
 	struct pech_core *cores;
 	uint32_t *lrs, *partials, *nzs;
+	int64_t *deltas;
 };
 
 static inline size_t pech_ws_align(size_t x) { return (x + 255u) & ~(size_t)255u; }
@@ -113,7 +115,7 @@ static inline size_t pech_ws_bytes(uint32_t m)
 {
 	const size_t nch = (m + PECH_CHUNK - 1u) / PECH_CHUNK, slots = nch * PECH_CHUNK;
 	return pech_ws_align(slots * sizeof(struct pech_core)) + pech_ws_align(slots * 4u) +
-	       2u * pech_ws_align(PECH_MAX_CHUNKS * 4u);
+	       2u * pech_ws_align(PECH_MAX_CHUNKS * 4u) + pech_ws_align(slots * 8u);
 }
 
 static inline struct pech_ws pech_ws_carve(void *base, uint32_t m)
@@ -128,6 +130,8 @@ static inline struct pech_ws pech_ws_carve(void *base, uint32_t m)
 	w.partials = (uint32_t *)p;
 	p += pech_ws_align(PECH_MAX_CHUNKS * 4u);
 	w.nzs = (uint32_t *)p;
+	p += pech_ws_align(PECH_MAX_CHUNKS * 4u);
+	w.deltas = (int64_t *)p;
 	return w;
 }
 

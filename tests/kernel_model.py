@@ -23,6 +23,7 @@ def _consts():
         out[m.group(1)] = int(m.group(2))
     ksrc = open(os.path.join(REPO, "pech_amd", "csrc", "crc32c_kernels.hip")).read()
     out["PECH_U"] = int(re.search(r"#define PECH_U (\d+)", ksrc).group(1))
+    out["PECH_U_COPY"] = int(re.search(r"#define PECH_U_COPY (\d+)", ksrc).group(1))
     out["PECH_MAIN_WAVES"] = int(re.search(r"#define PECH_MAIN_WAVES (\d+)", ksrc).group(1))
     out["PECH_SLOT_W"] = [int(re.search(r"#define PECH_SLOT_W%d (\d+)" % g, ksrc).group(1)) for g in range(4)]
     return out

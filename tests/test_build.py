@@ -38,7 +38,8 @@ def kernel_body(asm, name):
     return m.group(1)
 
 
-@pytest.mark.parametrize("kernel", ["pech_crc32c_plan", "pech_crc32c_main"])
+@pytest.mark.parametrize("kernel", ["pech_crc32c_plan", "pech_crc32c_main", "pech_crc32c_plan_copy",
+                                    "pech_crc32c_main_copy"])
 def test_no_calls_no_scratch(device_asm, kernel):
     asm, _ = device_asm
     body = kernel_body(asm, kernel)
@@ -46,9 +47,10 @@ def test_no_calls_no_scratch(device_asm, kernel):
     assert "scratch_" not in body and "buffer_store_dword" not in body, "register spill"
 
 
-def test_main_kernel_register_budget(device_asm):
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy"])
+def test_main_kernel_register_budget(device_asm, kernel):
     _, remarks = device_asm
-    m = re.search(r"Function Name: pech_crc32c_main.*?VGPRs: (\d+).*?ScratchSize \[bytes/lane\]: (\d+)", remarks,
+    m = re.search(r"Function Name: %s \[.*?VGPRs: (\d+).*?ScratchSize \[bytes/lane\]: (\d+)" % kernel, remarks,
                   flags=re.S)
     assert m, remarks[-1000:]
     vgprs, scratch = int(m.group(1)), int(m.group(2))
@@ -80,13 +82,13 @@ def _blocks(body):
     return out
 
 
-def test_row_loops_never_drain_the_ring(device_asm):
+def test_row_loops_never_drain_the_ring(device_asm, kernel="pech_crc32c_main"):
     """The row loops (basic blocks with a full block of Horner steps and
     their prefetch loads) keep PECH_U-1 loads in flight across the back
     edge: no vmcnt(0) and no ring-register copies (which is what a ring
     slot holding two live values compiles to -- found in the ISA of v0.3)."""
     asm, _ = device_asm
-    body = kernel_body(asm, "pech_crc32c_main")
+    body = kernel_body(asm, kernel)
     # every block holding a run of Horner steps with their prefetch loads
     loops = [(n, ins) for n, ins, note in _blocks(body)
              if sum(i.startswith("v_perm_b32") for i in ins) >= 64
@@ -97,3 +99,31 @@ def test_row_loops_never_drain_the_ring(device_asm):
         assert not waits, (name, waits)
         movs = [i for i in ins if i.startswith("v_mov_b32") or i.startswith("v_mov_b64")]
         assert len(movs) <= 8, (name, len(movs))
+
+
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy"])
+def test_loops_with_ring_loads_never_wait_for_zero(device_asm, kernel):
+    """Loop-level form of the check (the fused-copy kernel's loops span
+    several basic blocks): every loop -- from a "Loop Header" label to the
+    last branch back to it -- that issues ring loads has only counted
+    vmcnt waits."""
+    asm, _ = device_asm
+    lines = kernel_body(asm, kernel).split("\n")
+    heads = []  # (line, label): the header comment sits on the label's line or the next one
+    for i, l in enumerate(lines):
+        m = re.match(r"^(\.LBB\w+):", l)
+        if m and ("Loop Header" in l or (i + 1 < len(lines) and "Loop Header" in lines[i + 1]
+                                         and not lines[i + 1].lstrip().startswith("."))):
+            heads.append((i, m.group(1)))
+    checked = 0
+    for i0, label in heads:
+        pat = re.compile(r"^\s*s_(?:cbranch_\w+|branch)\s+%s\b" % re.escape(label))
+        back = [i for i, l in enumerate(lines) if i > i0 and pat.search(l)]
+        if not back:
+            continue
+        region = lines[i0:back[-1] + 1]
+        if sum("global_load_dwordx4" in l for l in region) < 4:
+            continue
+        checked += 1
+        assert not [l for l in region if "vmcnt(0)" in l], (kernel, label)
+    assert checked >= 1, (kernel, checked)  # the step loop, which holds every row loop

@@ -9,10 +9,10 @@ import pytest
 import kernel_model as KM
 
 
-def check(descs, ncu=4, seed=0, weights=None):
+def check(descs, ncu=4, seed=0, weights=None, U=None):
     rng = random.Random(seed)
     cores, lrs, partials, nzs = KM.plan(descs, rng)
-    ev = KM.main(cores, lrs, partials, nzs, ncu, weights=weights)
+    ev = KM.main(cores, lrs, partials, nzs, ncu, weights=weights, U=U)
     used = collections.Counter()
     byorig = {}
     for c in cores:
@@ -60,8 +60,9 @@ def test_tiny_and_unaligned():
     check(descs, ncu=3)
 
 
+@pytest.mark.parametrize("U", [None, KM.C["PECH_U_COPY"]])
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_mixed_sizes(seed):
+def test_mixed_sizes(seed, U):
     rng = random.Random(seed)
     sizes = [4096] * 200 + [65536] * 20 + [300000] * 3 + [16] * 30 + [7] * 10
     rng.shuffle(sizes)
@@ -69,7 +70,9 @@ def test_mixed_sizes(seed):
     for s in sizes:
         descs.append((base, s))
         base += s
-    check(descs, ncu=2, seed=seed)
+    # U: the fused-copy kernel's shallower ring too.  Its stores are exactly
+    # the non-virtual consumed pieces, so "used once" covers them
+    check(descs, ncu=2, seed=seed, U=U)
 
 
 def test_many_chunks_and_empty_chunks():

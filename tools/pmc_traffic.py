@@ -17,7 +17,7 @@ import sys
 def main():
     path, cfg, tag, out = sys.argv[1:5]
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if r["Kernel_Name"].startswith("pech_crc32c_main") and r["Counter_Name"] == "FETCH_SIZE"]
+            if r["Kernel_Name"] in ("pech_crc32c_main", "pech_crc32c_main_copy") and r["Counter_Name"] == "FETCH_SIZE"]
     if not vals:
         raise SystemExit("no pech_crc32c_main FETCH_SIZE rows")
     kib = sum(vals) / len(vals)
