@@ -199,20 +199,27 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	__shared__ uint32_t rows_at[PECH_CHUNK];
 	__shared__ uint32_t scratch[PECH_WAVES_PER_WG];
 	const uint32_t tid = threadIdx.x;
+	const uint32_t b = blockIdx.x * PECH_CHUNK + tid;
+	// All three loads unconditional (clamped indices) so they are in flight
+	// together: loads under exec-masked branches each got a vmcnt(0) at the
+	// branch's join -- three serial round trips before the first barrier.
+	pech_desc d = descs[min(b, n - 1u)];
+	const uint32_t tv1 = consts[PECH_C_TAB1 + (tid & 255u)];
+	const uint32_t tvp = consts[PECH_C_POWB + min(tid, 383u)];
+	if (b >= n)
+		d.len = 0;
 	if (tid < 256)
-		t1[tid] = consts[PECH_C_TAB1 + tid];
+		t1[tid] = tv1;
 	if (tid < 384)
-		powb[tid] = consts[PECH_C_POWB + tid];
+		powb[tid] = tvp;
 	if (tid < PECH_NCLASS)
 		hist[tid] = 0;
 	rows_at[tid] = 0;
 	__syncthreads();
 
-	const uint32_t b = blockIdx.x * PECH_CHUNK + tid;
 	uint32_t rows = 0, cls = 0;
 	pech_core core = {0, 0, 0};
 	if (b < n) {
-		const pech_desc d = descs[b];
 		const uint64_t end = d.addr + d.len;
 		rows = pech_core_rows(d.addr, d.len);
 		uint32_t res;
@@ -356,14 +363,16 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 #define LD_PIECE(S, a, tag) (__builtin_nontemporal_load((g_u32x4 *)(a)))
 #endif
 
-// Locate row r of the batch's row space: chunk by binary search of the LDS
-// prefix, then an SG-ary search of the chunk's row offsets by the SG lanes of
-// a sub-group (lanes [sgbase, sgbase+SG) of the wave, all with the same r).
-// Returns the position (plan order) and the row inside that buffer.
-template <uint32_t SG>
-__device__ __forceinline__ void find_start(const uint32_t *__restrict__ lrs, const uint32_t *lds, uint32_t nchunks,
-					   uint32_t r, uint32_t sl, uint32_t sgbase, bool want, uint32_t &pos,
-					   uint32_t &lr)
+// Locate row r of the batch's row space in ONE global round: the chunk by
+// binary search of the LDS prefix, then the whole wave reads the chunk's
+// PECH_CHUNK row offsets (16 per lane, four 16-byte loads) and counts those
+// <= the chunk-local row (they are nondecreasing, strictly over the chunk's
+// nz non-empty cores).  Returns the position (plan order) and the row inside
+// that buffer, wave-uniform.
+static_assert(PECH_CHUNK == 64u * 16u, "find_start_wave: 16 row offsets per lane");
+__device__ __forceinline__ void find_start_wave(const uint32_t *__restrict__ lrs, const uint32_t *lds,
+						uint32_t nchunks, uint32_t r, uint32_t lane, uint32_t &pos,
+						uint32_t &lr)
 {
 	uint32_t clo = 0, chi = nchunks;
 	while (chi - clo > 1) {
@@ -374,23 +383,28 @@ __device__ __forceinline__ void find_start(const uint32_t *__restrict__ lrs, con
 			chi = mid;
 	}
 	const uint32_t rr = r - lds[L_CHUNK / 4u + clo];
-	uint32_t plo = clo * PECH_CHUNK, phi = plo + lds[L_NZ / 4u + clo];
-	bool active = want && phi - plo > 1;
-	while (__any(active)) {
-		const uint32_t step = (phi - plo + SG - 1u) / SG;
-		const uint32_t p = plo + sl * step;
-		const bool ok = active && p < phi && lrs[p] <= rr;
-		const uint64_t bal = __ballot(ok);
-		const uint64_t mask = SG >= 64 ? ~0ull : ((1ull << (SG & 63u)) - 1ull);
-		const uint32_t cnt = (uint32_t)__popcll((bal >> sgbase) & mask);
-		if (active) {
-			plo = plo + (cnt - 1u) * step;
-			phi = min(phi, plo + step);
-			active = phi - plo > 1;
+	const uint32_t nz = lds[L_NZ / 4u + clo];
+	const u32x4 *src = (const u32x4 *)(lrs + clo * PECH_CHUNK + lane * 16u);
+	uint32_t cnt = 0, lo = 0;
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k) {
+		const u32x4 v = src[k];
+		const uint32_t i0 = lane * 16u + 4u * k;
+		const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+		for (uint32_t j = 0; j < 4; ++j) {
+			const bool ok = i0 + j < nz && e[j] <= rr;
+			cnt += ok ? 1u : 0u;
+			lo = ok ? max(lo, e[j]) : lo;
 		}
 	}
-	pos = plo;
-	lr = want ? rr - lrs[plo] : 0u;
+#pragma unroll
+	for (uint32_t d = 1; d < 64; d <<= 1) {
+		cnt += __shfl_xor(cnt, d);
+		lo = max(lo, (uint32_t)__shfl_xor(lo, d));
+	}
+	pos = uni(clo * PECH_CHUNK + cnt - 1u);
+	lr = uni(rr - lo);
 }
 
 // s_setprio takes an immediate: wave-uniform branch over the 4 levels
@@ -662,6 +676,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 {
 	const uint32_t tid = threadIdx.x;
 	STAMP(t_entry);
+#ifdef PECH_PROLOGUE_PRIO // A/B: prologue at raised issue priority, back to 0 for the row loops
+	__builtin_amdgcn_s_setprio(3);
+#endif
 
 	// Table constants first: their loads (L2/MALL) overlap the chunk-count
 	// loads below, and the LDS fill is done before the scan's barriers --
@@ -741,12 +758,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * slot_cw(wave + 1u) / slot_cw(PECH_MAIN_WAVES));
 	const uint32_t rem_all = r1 - r0;
 	uint32_t p0 = 0, lr0 = 0;
-	if (rem_all) {
-		uint32_t pos, lr;
-		find_start<64>(lrs, lds, nchunks, r0, lane, 0u, true, pos, lr);
-		p0 = uni(pos);
-		lr0 = uni(lr);
-	}
+	if (rem_all)
+		find_start_wave(lrs, lds, nchunks, r0, lane, p0, lr0);
 	STAMP(t_find);
 	Step S = plan_step<COPY>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp);
 	STAMP(t_plan);
@@ -754,9 +767,17 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		RING_PRIME(S, ring);
 
 	STAMP(t_fill);
-	__syncthreads(); // tables (written before the scan) and the ring prime
+	// No barrier here: the LDS tables were written before the scan's
+	// barriers, and the ring is the wave's own.  Each wave starts streaming
+	// as soon as its prime is issued (a barrier cost 1-2 us of prologue).
 
 	STAMP(t_start);
+#ifdef PECH_PROLOGUE_PRIO
+	__builtin_amdgcn_s_setprio(0);
+#endif
+#ifdef PECH_PRELOOP_BARRIER // A/B: every wave of the workgroup primed before any streams
+	__syncthreads();
+#endif
 #ifdef PECH_PRIO_YOUNG // diagnostic: younger waves (higher age rank on the SIMD) issue first
 	set_prio(wave >> 2);
 #endif
@@ -891,6 +912,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.7 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.8 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }

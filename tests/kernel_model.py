@@ -144,9 +144,10 @@ def run_rows_loads(U, nl, nu, zoff, T, nmin):
     return loads, consumed
 
 
-def find_start(lrs, pref, nzs, r, SG):
-    """find_start<SG>: chunk by binary search, then SG-ary search (as the
-    kernel's lanes do it)."""
+def find_start(lrs, pref, nzs, r):
+    """find_start_wave: chunk by binary search of the prefix, then the count
+    of the chunk's row offsets <= the chunk-local row (one wave-wide read of
+    all PECH_CHUNK offsets, entries past nz excluded)."""
     nchunks = len(nzs)
     clo, chi = 0, nchunks
     while chi - clo > 1:
@@ -156,13 +157,9 @@ def find_start(lrs, pref, nzs, r, SG):
         else:
             chi = mid
     rr = r - pref[clo]
-    plo, phi = clo * CHUNK, clo * CHUNK + nzs[clo]
-    while phi - plo > 1:
-        step = (phi - plo + SG - 1) // SG
-        cnt = sum(1 for sl in range(SG) if plo + sl * step < phi and lrs[plo + sl * step] <= rr)
-        plo = plo + (cnt - 1) * step
-        phi = min(phi, plo + step)
-    return plo, rr - lrs[plo]
+    ok = [lrs[clo * CHUNK + i] for i in range(CHUNK) if i < nzs[clo] and lrs[clo * CHUNK + i] <= rr]
+    assert ok, "row offset 0 always qualifies"
+    return clo * CHUNK + len(ok) - 1, rr - max(ok)
 
 
 def slot_cw(k, weights):
@@ -202,7 +199,7 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
     events = []
     for r0, r1 in wave_ranges(Rtot, ncu, rpw_min, weights):
         if r1 > r0:
-            pos, lr = find_start(lrs, pref, nzs, r0, 64)
+            pos, lr = find_start(lrs, pref, nzs, r0)
             walk(cores, nzs, pos, lr, r1 - r0, U, events)
     return events
 

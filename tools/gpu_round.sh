@@ -5,6 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 stop() { echo "stopping after rc=$1 ($2)"; exit "$1"; }
+if [ -z "${SKIP_TESTS:-}" ]; then
 PECH_CRC32C_LIB=build/lib_dbg.so timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 \
   --timeout-method thread > gpurun_out/pytest_dbg.log 2>&1 || { tail -30 gpurun_out/pytest_dbg.log; stop $? dbg; }
 echo "dbg: $(tail -1 gpurun_out/pytest_dbg.log) oob=$(grep -c 'PECH OOB' gpurun_out/pytest_dbg.log)"
@@ -12,8 +13,9 @@ grep -q "PECH OOB" gpurun_out/pytest_dbg.log && stop 1 oob
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; stop $? pytest; }
 echo "release: $(tail -1 gpurun_out/pytest_gpu.log)"
+fi
 for cfg in ${STAMP_CONFIGS:-}; do
-  PECH_CRC32C_LIB=build/lib_stamps.so timeout -k 10 120 python tools/wave_stamps.py $cfg > gpurun_out/stamps_$cfg.txt 2>&1 \
+  PECH_CRC32C_LIB=${STAMP_LIB:-build/lib_stamps.so} timeout -k 10 120 python tools/wave_stamps.py $cfg > gpurun_out/stamps_$cfg.txt 2>&1 \
     || stop $? "stamps $cfg"
   grep -v "amdgpu.ids\|^xcc\|histogram" gpurun_out/stamps_$cfg.txt
 done
