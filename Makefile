@@ -41,8 +41,9 @@ variant: build/crc32c_api.o build/crc32c_async.o
 # links the test oracle for the expected footer CRCs -- not product code
 build/msgr_sim: tests/c/msgr_sim.c oracle/crc32c_oracle.c include/pech_crc32c_async.h $(LIB)
 	@mkdir -p build
-	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude tests/c/msgr_sim.c oracle/crc32c_oracle.c \
-		-Lpech_amd -lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
+	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+		tests/c/msgr_sim.c oracle/crc32c_oracle.c -Lpech_amd -lpech_crc32c -L/opt/rocm/lib -lamdhip64 \
+		-Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
 
 oracle:
 	$(MAKE) -C oracle all

@@ -76,7 +76,10 @@ typedef void (*crc32c_done_fn)(void *arg, uint32_t crc, int err);
 #define CRC32C_ASYNC_ZEROCOPY 1u
 
 /* A context on the current device: its own HIP stream, staging slots and
- * eventfd.  NULL on failure. */
+ * eventfd.  NULL on failure.  Every later call on the context runs on that
+ * device and restores the caller's current device, so one thread can drive
+ * one context per GPU (independent payloads shard over GPUs with no
+ * collective). */
 struct crc32c_async *crc32c_async_create(unsigned int flags);
 
 /* The eventfd (EFD_NONBLOCK | EFD_CLOEXEC): readable while finished batches

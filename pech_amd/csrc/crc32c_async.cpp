@@ -153,6 +153,25 @@ static uint64_t pinned_dev_addr(const void *p, size_t len)
 // async contexts
 namespace {
 
+// Every entry point runs on its context's device and restores the caller's:
+// one thread can drive one context per GPU without
+// tracking the current device itself.
+struct DeviceGuard {
+	int prev = -1;
+	bool ok = false;
+	explicit DeviceGuard(int dev)
+	{
+		if (hipGetDevice(&prev) != hipSuccess)
+			return;
+		ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+	}
+	~DeviceGuard()
+	{
+		if (ok && prev >= 0)
+			(void)hipSetDevice(prev);
+	}
+};
+
 constexpr size_t kSlotBytes = 32u << 20; // staging per slot
 constexpr uint32_t kSlotDescs = 8192;    // descriptors per slot
 constexpr unsigned kMaxSlots = 4;        // slots in flight per context
@@ -378,6 +397,11 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 	}
 	if (a->err)
 		return a->err;
+	DeviceGuard dg(a->dev);
+	if (!dg.ok) {
+		pech_internal_set_err("crc32c_async_submit: cannot select device %d", a->dev);
+		return -ENODEV;
+	}
 	const uint64_t id = a->base + a->items.size();
 	a->items.push_back(Item{done, arg, seed, 0u, 0u, false, 0});
 	const uint8_t *p = (const uint8_t *)buf;
@@ -437,6 +461,7 @@ extern "C" int crc32c_async_flush(struct crc32c_async *a)
 		return -EINVAL;
 	if (a->err)
 		return a->err;
+	DeviceGuard dg(a->dev);
 	return launch_slot(a);
 }
 
@@ -461,6 +486,7 @@ extern "C" int crc32c_async_complete(struct crc32c_async *a)
 {
 	if (!a)
 		return -EINVAL;
+	DeviceGuard dg(a->dev);
 	uint64_t cnt;
 	while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
 	}
@@ -473,6 +499,7 @@ extern "C" int crc32c_async_drain(struct crc32c_async *a)
 {
 	if (!a)
 		return -EINVAL;
+	DeviceGuard dg(a->dev);
 	int rc = a->err ? a->err : launch_slot(a);
 	while (!a->inflight.empty()) {
 		int r = reap(a, true);
@@ -495,6 +522,7 @@ extern "C" void crc32c_async_destroy(struct crc32c_async *a)
 {
 	if (!a)
 		return;
+	DeviceGuard dg(a->dev >= 0 ? a->dev : 0);
 	if (a->stream) {
 		(void)crc32c_async_drain(a);
 		(void)hipStreamSynchronize(a->stream);

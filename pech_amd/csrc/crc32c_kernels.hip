@@ -663,8 +663,13 @@ template <bool COPY>
 __device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, bool ok)
 {
 	typedef __attribute__((address_space(1))) u32x4 g_u32x4w;
+#ifdef PECH_TEMPORAL_STORES // A/B: default cache policy for the copy's stores
+	if (COPY && ok)
+		*(g_u32x4w *)(S.dad + (uint64_t)row * PECH_ROW_BYTES) = v;
+#else
 	if (COPY && ok)
 		__builtin_nontemporal_store(v, (g_u32x4w *)(S.dad + (uint64_t)row * PECH_ROW_BYTES));
+#endif
 }
 
 template <bool COPY, uint32_t U>

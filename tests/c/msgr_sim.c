@@ -15,16 +15,19 @@
  *     reference per-piece chain (oracle_crc32c_pieces, the test oracle).
  *   - the event loop (src/event.c:52-70): epoll_wait on the context's
  *     eventfd, as an event_item would (include/event.h:7-28).
+ *   - several GPUs from pech's one thread: argv[3] contexts,
+ *     context k created on device k % device-count, messages dealt round
+ *     robin, one eventfd each on the same epoll set.
  * Exit status 0 iff every message verified and none is left pending.
  *
- * Build (tests/test_async.py does it):
- *   gcc -std=gnu89 -O2 -Iinclude tests/c/msgr_sim.c oracle/crc32c_oracle.c \
- *       -Lpech_amd -lpech_crc32c -Wl,-rpath,$PWD/pech_amd -o build/msgr_sim
+ * Build: `make build/msgr_sim` (part of `make all`; gnu89, -Wall -Werror).
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
+
+#include <hip/hip_runtime_api.h>
 
 #include "pech_crc32c_async.h"
 
@@ -79,25 +82,40 @@ int main(int argc, char **argv)
 					     (40 << 20) + 17};
 	unsigned int nmsgs = argc > 1 ? (unsigned int)atoi(argv[1]) : 300;
 	unsigned int zerocopy = argc > 2 ? (unsigned int)atoi(argv[2]) : 0;
-	struct crc32c_async *a;
-	struct epoll_event ev, out;
+	unsigned int nctx = argc > 3 ? (unsigned int)atoi(argv[3]) : 1;
+	struct crc32c_async *ctxs[16], *a;
+	struct epoll_event ev, out[16];
 	struct msg *msgs;
-	unsigned int i, k;
-	int ep, rc;
+	unsigned int i, k, c;
+	int ep, rc, ndev = 1;
 
-	a = crc32c_async_create(zerocopy ? CRC32C_ASYNC_ZEROCOPY : CRC32C_ASYNC_DEFAULT);
-	if (!a) {
-		fprintf(stderr, "crc32c_async_create: %s\n", crc32c_last_error());
+	if (nctx < 1 || nctx > 16)
 		return 2;
-	}
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+		ndev = 1;
 	ep = epoll_create1(0);
-	memset(&ev, 0, sizeof(ev));
-	ev.events = EPOLLIN;
-	ev.data.fd = crc32c_async_fd(a);
-	if (ep < 0 || epoll_ctl(ep, EPOLL_CTL_ADD, ev.data.fd, &ev)) {
-		perror("epoll");
+	if (ep < 0) {
+		perror("epoll_create1");
 		return 2;
 	}
+	for (c = 0; c < nctx; c++) {
+		/* the context keeps the device current at creation */
+		if (hipSetDevice((int)(c % (unsigned int)ndev)) != hipSuccess)
+			return 2;
+		ctxs[c] = crc32c_async_create(zerocopy ? CRC32C_ASYNC_ZEROCOPY : CRC32C_ASYNC_DEFAULT);
+		if (!ctxs[c]) {
+			fprintf(stderr, "crc32c_async_create: %s\n", crc32c_last_error());
+			return 2;
+		}
+		memset(&ev, 0, sizeof(ev));
+		ev.events = EPOLLIN;
+		ev.data.u32 = c;
+		if (epoll_ctl(ep, EPOLL_CTL_ADD, crc32c_async_fd(ctxs[c]), &ev)) {
+			perror("epoll_ctl");
+			return 2;
+		}
+	}
+	(void)hipSetDevice(0); /* the contexts switch devices themselves */
 	msgs = calloc(nmsgs, sizeof(*msgs));
 	for (i = 0; i < nmsgs; i++) {
 		struct msg *m = &msgs[i];
@@ -119,6 +137,7 @@ int main(int argc, char **argv)
 			m->data[k] = next_byte();
 		m->footer_data_crc = oracle_crc32c_pieces(0, m->data, m->data_len, 4096);
 		/* total_resid == 0: one submission for the whole payload */
+		a = ctxs[i % nctx];
 		rc = crc32c_async_submit(a, m->data, m->data_len, 0, data_crc_done, m);
 		if (rc) {
 			fprintf(stderr, "submit: %d %s\n", rc, crc32c_last_error());
@@ -133,26 +152,34 @@ int main(int argc, char **argv)
 		if (i % 5 == 0 && crc32c_async_complete(a) < 0)
 			return 2;
 	}
-	if ((rc = crc32c_async_flush(a))) {
-		fprintf(stderr, "flush: %d %s\n", rc, crc32c_last_error());
-		return 2;
-	}
-	/* the event loop: wait for the eventfd, complete, until nothing pending */
-	while (crc32c_async_pending(a)) {
-		int n = epoll_wait(ep, &out, 1, 10000);
+	for (c = 0; c < nctx; c++)
+		if ((rc = crc32c_async_flush(ctxs[c]))) {
+			fprintf(stderr, "flush: %d %s\n", rc, crc32c_last_error());
+			return 2;
+		}
+	/* the event loop: wait for an eventfd, complete it, until nothing pending */
+	for (;;) {
+		unsigned int pending = 0;
+		int n, j;
 
+		for (c = 0; c < nctx; c++)
+			pending += crc32c_async_pending(ctxs[c]);
+		if (!pending)
+			break;
+		n = epoll_wait(ep, out, 16, 10000);
 		if (n < 0) {
 			perror("epoll_wait");
 			return 2;
 		}
 		if (n == 0) {
-			fprintf(stderr, "timeout: %u pending\n", crc32c_async_pending(a));
+			fprintf(stderr, "timeout: %u pending\n", pending);
 			return 3;
 		}
-		if (crc32c_async_complete(a) < 0) {
-			fprintf(stderr, "complete: %s\n", crc32c_last_error());
-			return 2;
-		}
+		for (j = 0; j < n; j++)
+			if (crc32c_async_complete(ctxs[out[j].data.u32]) < 0) {
+				fprintf(stderr, "complete: %s\n", crc32c_last_error());
+				return 2;
+			}
 	}
 	for (i = 0; i < nmsgs; i++) {
 		if (!msgs[i].verified)
@@ -162,8 +189,10 @@ int main(int argc, char **argv)
 		else
 			crc32c_pages_free(msgs[i].data, msgs[i].order);
 	}
-	crc32c_async_destroy(a);
+	for (c = 0; c < nctx; c++)
+		crc32c_async_destroy(ctxs[c]);
 	crc32c_pages_trim();
-	printf("msgr_sim: %u messages, %u verified, %u bad (zerocopy %u)\n", nmsgs, nr_done, nr_bad, zerocopy);
+	printf("msgr_sim: %u messages, %u verified, %u bad (zerocopy %u, %u contexts on %d device(s))\n", nmsgs,
+	       nr_done, nr_bad, zerocopy, nctx, ndev);
 	return nr_bad ? 1 : 0;
 }

@@ -138,10 +138,12 @@ def test_pages_allocator():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zerocopy", ["0", "1"])
-def test_msgr_sim_event_loop(zerocopy):
+@pytest.mark.parametrize("zerocopy,contexts", [("0", "1"), ("1", "1"), ("1", "3")])
+def test_msgr_sim_event_loop(zerocopy, contexts):
+    # contexts > 1: one context per GPU in turn (several per GPU on a 1-GPU
+    # box), all driven from one thread on one epoll set
     exe = os.path.join(REPO, "build", "msgr_sim")
     assert os.path.exists(exe), "build/msgr_sim is built by `make` (__graft_entry__.build())"
-    r = subprocess.run([exe, "200", zerocopy], capture_output=True, timeout=120)
+    r = subprocess.run([exe, "200", zerocopy, contexts], capture_output=True, timeout=120)
     assert r.returncode == 0, (r.stdout.decode(), r.stderr.decode())
     assert b"0 bad" in r.stdout

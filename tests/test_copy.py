@@ -1,0 +1,100 @@
+"""Fused CRC + copy (crc32c_dev_copy_batch_*, SURVEY §8f row 4: the copies
+memstore makes of the same bytes, src/ceph/memstore.c:306, :445): every CRC
+bit-exact against the oracle, every destination byte equal to its source,
+and not one byte outside the destination ranges written (guard pattern)."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+GUARD = 0xA5
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return torch, torch.device("cuda:0")
+
+
+def run_copy(torch, dev, host_src, src_offs, lens, dst_offs, dst_bytes, seeds=None):
+    import pech_amd as P
+    from pech_amd import _lib
+
+    src = torch.from_numpy(host_src).to(dev)
+    dst = torch.full((dst_bytes,), GUARD, dtype=torch.uint8, device=dev)
+    descs = P.make_descs(src.data_ptr() + np.asarray(src_offs, dtype=np.int64), lens, seeds, device=dev)
+    dsts = torch.from_numpy((dst.data_ptr() + np.asarray(dst_offs, dtype=np.int64)).astype(np.int64)).to(dev)
+    out = torch.zeros(len(lens), dtype=torch.int32, device=dev)
+    rc = _lib.lib().crc32c_dev_copy_batch_async(descs.data_ptr(), dsts.data_ptr(), out.data_ptr(), len(lens),
+                                                 torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(rc, "crc32c_dev_copy_batch_async")
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32), dst.cpu().numpy()
+
+
+def check_copy(host_src, src_offs, lens, dst_offs, got_dst):
+    mask = np.zeros(got_dst.size, dtype=bool)
+    for so, n, do in zip(src_offs, lens, dst_offs):
+        so, n, do = int(so), int(n), int(do)
+        assert np.array_equal(got_dst[do:do + n], host_src[so:so + n]), (so, n, do)
+        mask[do:do + n] = True
+    outside = got_dst[~mask]
+    assert np.all(outside == GUARD), f"{int(np.count_nonzero(outside != GUARD))} bytes written outside destinations"
+
+
+def test_copy_random_unaligned(torch_dev):
+    # random lengths (tiny ones included), sources and destinations at
+    # unrelated byte alignments, gaps between destinations to catch stray writes
+    torch, dev = torch_dev
+    rng = np.random.default_rng(77)
+    n = 1500
+    lens = rng.integers(0, 70000, n)
+    tiny = rng.random(n) < 0.15
+    lens[tiny] = rng.integers(0, 40, int(tiny.sum()))
+    src_offs, dst_offs = np.zeros(n, np.int64), np.zeros(n, np.int64)
+    sp = dp = 0
+    for i in range(n):
+        sp += int(rng.integers(0, 48))
+        dp += int(rng.integers(1, 48))
+        src_offs[i], dst_offs[i] = sp, dp
+        sp += int(lens[i])
+        dp += int(lens[i])
+    host = rng.integers(0, 256, sp + 64, dtype=np.uint8)
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+    got, dst = run_copy(torch, dev, host, src_offs, lens, dst_offs, dp + 64, seeds)
+    assert np.array_equal(got, O.crcs(host, src_offs, lens, seeds))
+    check_copy(host, src_offs, lens, dst_offs, dst)
+
+
+@pytest.mark.parametrize("shape", ["c2", "c3", "c4"])
+def test_copy_bench_shapes(torch_dev, shape):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(3)
+    if shape == "c2":
+        lens = [4096] * 16384
+    elif shape == "c3":
+        lens = [4 << 20] * 16
+    else:
+        lens = [4096] * 4096 + [65536] * 256 + [1 << 20] * 16 + [4 << 20] * 4
+        rng.shuffle(lens)
+    lens = np.asarray(lens, np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    host = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    dst_offs = offs + 4096 * np.arange(len(lens))  # a guard page between destinations
+    got, dst = run_copy(torch, dev, host, offs, lens, dst_offs, int(dst_offs[-1] + lens[-1] + 4096))
+    assert np.array_equal(got, O.crcs(host, offs, lens))
+    check_copy(host, offs, lens, dst_offs, dst)
+
+
+def test_copy_huge_buffer_misaligned(torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(4)
+    L = (40 << 20) + 12345
+    host = rng.integers(0, 256, L + 64, dtype=np.uint8)
+    got, dst = run_copy(torch, dev, host, [3], [L], [11], L + 64, [0x12345678])
+    assert int(got[0]) == O.crc(0x12345678, host[3:3 + L])
+    check_copy(host, [3], [L], [11], dst)
