@@ -373,9 +373,26 @@ def cpu_baseline(args, buf0, offs, sizes, outs, rotate, P):
                 break
     except OSError:
         pass
-    return {"value": round(done_bytes / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+    rate1 = done_bytes / dt / (1 << 30)
+    line = {"value": round(rate1, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": f"{k} leading buffers ({nbytes / (1 << 20):.0f} MiB) of batch 0, {reps} pass(es), "
                       f"{dt:.1f} s, 1 thread, {cpu_model}; GPU outputs for the sample matched bit-exact"}
+    # the same reference loop on this GPU's share of host cores (16 per GPU on
+    # the box), independent buffers split over POSIX threads
+    if ref is not None and hasattr(ref, "ref_crc32c_batch_mt"):
+        threads = max(1, min(16, os.cpu_count() or 1))
+        c_offs = np.ascontiguousarray(offs[:k], dtype=np.uint64)
+        c_lens = np.ascontiguousarray(sizes[:k], dtype=np.uint32)
+        mres = np.zeros(k, dtype=np.uint32)
+        mreps = max(1, int(args.cpu_seconds / 3 * threads * rate1 * (1 << 30) / nbytes))
+        t0 = time.perf_counter()
+        rc = ref.ref_crc32c_batch_mt(base, c_offs.ctypes.data, c_lens.ctypes.data, mres.ctypes.data, k, threads,
+                                     mreps)
+        mdt = time.perf_counter() - t0
+        if rc == 0 and np.array_equal(mres, res):
+            line["multi_thread"] = {"value": round(nbytes * mreps / mdt / (1 << 30), 3), "unit": "GiB/s",
+                                    "threads": threads, "passes": mreps, "seconds": round(mdt, 2)}
+    return line
 
 
 if __name__ == "__main__":

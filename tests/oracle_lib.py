@@ -51,6 +51,10 @@ def ref():
         L.ref_crc32c.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint]
         L.ref_table_copy.restype = None
         L.ref_table_copy.argtypes = [ctypes.c_void_p]
+        if hasattr(L, "ref_crc32c_batch_mt"):
+            L.ref_crc32c_batch_mt.restype = ctypes.c_int
+            L.ref_crc32c_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]
         L.ref_crc32c_strided.restype = None
         L.ref_crc32c_strided.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_void_p,
                                          ctypes.c_uint]
