@@ -1,7 +1,8 @@
 // crc32c_async.cpp -- the messenger-facing layer (include/pech_crc32c_async.h):
 // pinned payload pages, eventfd-completed payload batches, concatenation.
 //
-// Data path of one async context (one HIP stream):
+// Data path of one async context (up to four staging slots in flight, each
+// with its own HIP stream and workspace, so small batches overlap):
 //   submit()   places the payload in the slot being filled -- pageable bytes
 //              are packed into the slot's pinned staging buffer (one CPU
 //              copy), crc32c_pages bytes are DMA'd straight from where they
@@ -182,6 +183,8 @@ struct Piece {
 };
 
 struct Slot {
+	hipStream_t stream = nullptr; // own stream and workspace: up to kMaxSlots batches overlap
+	void *d_ws = nullptr;
 	uint8_t *h_stage = nullptr, *d_stage = nullptr;
 	pech_desc *h_desc = nullptr, *d_desc = nullptr;
 	uint32_t *h_out = nullptr, *d_out = nullptr;
@@ -207,10 +210,8 @@ struct Item {
 struct crc32c_async {
 	int dev = -1;
 	unsigned flags = 0;
-	hipStream_t stream = nullptr;
 	int efd = -1;
-	void *d_ws = nullptr;
-	size_t ws_bytes = 0;
+	bool ready = false; // fully created (destroy drains only then)
 	std::vector<Slot *> slots;
 	std::deque<Slot *> inflight; // launch order
 	Slot *cur = nullptr;         // slot being filled
@@ -221,6 +222,12 @@ struct crc32c_async {
 
 static void slot_free(Slot *s)
 {
+	if (s->stream) {
+		(void)hipStreamSynchronize(s->stream);
+		(void)hipStreamDestroy(s->stream);
+	}
+	if (s->d_ws)
+		(void)hipFree(s->d_ws);
 	if (s->h_stage)
 		(void)hipHostFree(s->h_stage);
 	if (s->d_stage)
@@ -241,7 +248,9 @@ static void slot_free(Slot *s)
 static Slot *slot_new(void)
 {
 	Slot *s = new Slot();
-	if (hipHostMalloc(&s->h_stage, kSlotBytes, hipHostMallocDefault) != hipSuccess ||
+	if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipMalloc(&s->d_ws, pech_ws_bytes(kSlotDescs)) != hipSuccess ||
+	    hipHostMalloc(&s->h_stage, kSlotBytes, hipHostMallocDefault) != hipSuccess ||
 	    hipMalloc(&s->d_stage, kSlotBytes) != hipSuccess ||
 	    hipHostMalloc(&s->h_desc, kSlotDescs * sizeof(pech_desc), hipHostMallocDefault) != hipSuccess ||
 	    hipMalloc(&s->d_desc, kSlotDescs * sizeof(pech_desc)) != hipSuccess ||
@@ -341,15 +350,15 @@ static int launch_slot(crc32c_async *a)
 	const unsigned m = (unsigned)s->pieces.size();
 	for (auto &r : s->packed)
 		TRY_HIP(hipMemcpyAsync(s->d_stage + r.first, s->h_stage + r.first, r.second - r.first,
-				       hipMemcpyHostToDevice, a->stream),
+				       hipMemcpyHostToDevice, s->stream),
 			-EIO);
-	TRY_HIP(hipMemcpyAsync(s->d_desc, s->h_desc, m * sizeof(pech_desc), hipMemcpyHostToDevice, a->stream), -EIO);
-	int rc = pech_internal_launch(s->d_desc, s->d_out, m, a->d_ws, a->ws_bytes, a->stream);
+	TRY_HIP(hipMemcpyAsync(s->d_desc, s->h_desc, m * sizeof(pech_desc), hipMemcpyHostToDevice, s->stream), -EIO);
+	int rc = pech_internal_launch(s->d_desc, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream);
 	if (rc)
 		return rc;
-	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, a->stream), -EIO);
-	TRY_HIP(hipEventRecord(s->done, a->stream), -EIO);
-	TRY_HIP(hipLaunchHostFunc(a->stream, host_notify, &a->efd), -EIO);
+	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), -EIO);
+	TRY_HIP(hipEventRecord(s->done, s->stream), -EIO);
+	TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, &a->efd), -EIO);
 	s->inflight = true;
 	a->inflight.push_back(s);
 	a->cur = nullptr;
@@ -366,10 +375,7 @@ extern "C" struct crc32c_async *crc32c_async_create(unsigned int flags)
 		return nullptr;
 	crc32c_async *a = new crc32c_async();
 	a->flags = flags;
-	a->ws_bytes = pech_ws_bytes(kSlotDescs);
-	if (hipGetDevice(&a->dev) != hipSuccess ||
-	    hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess ||
-	    hipMalloc(&a->d_ws, a->ws_bytes) != hipSuccess) {
+	if (hipGetDevice(&a->dev) != hipSuccess) {
 		pech_internal_set_err("crc32c_async_create: %s", hipGetErrorString(hipGetLastError()));
 		crc32c_async_destroy(a);
 		return nullptr;
@@ -380,6 +386,7 @@ extern "C" struct crc32c_async *crc32c_async_create(unsigned int flags)
 		crc32c_async_destroy(a);
 		return nullptr;
 	}
+	a->ready = true;
 	return a;
 }
 
@@ -428,7 +435,7 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 			piece = left < kSlotBytes - s->used ? left : kSlotBytes - s->used;
 			d.addr = (uint64_t)(uintptr_t)(s->d_stage + s->used);
 			if (piece && dma) {
-				TRY_HIP(hipMemcpyAsync(s->d_stage + s->used, p, piece, hipMemcpyHostToDevice, a->stream),
+				TRY_HIP(hipMemcpyAsync(s->d_stage + s->used, p, piece, hipMemcpyHostToDevice, s->stream),
 					-EIO);
 			} else if (piece) {
 				memcpy(s->h_stage + s->used, p, piece);
@@ -523,16 +530,10 @@ extern "C" void crc32c_async_destroy(struct crc32c_async *a)
 	if (!a)
 		return;
 	DeviceGuard dg(a->dev >= 0 ? a->dev : 0);
-	if (a->stream) {
+	if (a->ready)
 		(void)crc32c_async_drain(a);
-		(void)hipStreamSynchronize(a->stream);
-	}
 	for (Slot *s : a->slots)
-		slot_free(s);
-	if (a->d_ws)
-		(void)hipFree(a->d_ws);
-	if (a->stream)
-		(void)hipStreamDestroy(a->stream);
+		slot_free(s); // synchronises the slot's stream first
 	if (a->efd >= 0)
 		close(a->efd);
 	delete a;

@@ -20,12 +20,20 @@
  *     robin, one eventfd each on the same epoll set.
  * Exit status 0 iff every message verified and none is left pending.
  *
+ * Bench mode (bench.py's msgr_async leg for small payloads):
+ *   msgr_sim bench <payload bytes> <count> <zerocopy> <passes>
+ * submits <count> payloads of crc32c_pages memory per pass (carved from
+ * order-11 blocks), flushing every 64, and drains through the eventfd; checks
+ * every result of the first pass against the oracle, then prints one JSON
+ * line with GiB/s and payloads/s over the timed passes.
+ *
  * Build: `make build/msgr_sim` (part of `make all`; gnu89, -Wall -Werror).
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -76,6 +84,80 @@ static unsigned char next_byte(void)
 	return (unsigned char)xs;
 }
 
+struct bench_slot {
+	uint32_t want, got;
+	int err;
+};
+
+static void bench_done(void *arg, uint32_t crc, int err)
+{
+	struct bench_slot *b = arg;
+
+	b->got = crc;
+	b->err = err;
+}
+
+static double now_s(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int bench_main(unsigned int size, unsigned int count, unsigned int zerocopy, unsigned int passes)
+{
+	const size_t block = (size_t)CRC32C_PAGE_SIZE << 11;
+	const size_t stride = ((size_t)size + 255u) & ~(size_t)255u;
+	const unsigned int per_block = (unsigned int)(block / (stride ? stride : 256u));
+	unsigned int nblocks = (count + per_block - 1) / per_block, i, p, bad = 0;
+	unsigned char **blocks = calloc(nblocks, sizeof(*blocks));
+	struct bench_slot *slots = calloc(count, sizeof(*slots));
+	struct crc32c_async *a = crc32c_async_create(zerocopy ? CRC32C_ASYNC_ZEROCOPY : CRC32C_ASYNC_DEFAULT);
+	double t0 = 0, t1;
+
+	if (!a || !blocks || !slots || !per_block)
+		return 2;
+	for (i = 0; i < nblocks; i++) {
+		size_t k;
+
+		blocks[i] = crc32c_pages_alloc(11);
+		if (!blocks[i])
+			return 2;
+		for (k = 0; k < block; k++)
+			blocks[i][k] = next_byte();
+	}
+	for (i = 0; i < count; i++)
+		slots[i].want = oracle_crc32c_pieces(0, blocks[i / per_block] + (size_t)(i % per_block) * stride, size,
+						     4096);
+	for (p = 0; p <= passes; p++) {
+		if (p == 1)
+			t0 = now_s(); /* pass 0 is the warm-up */
+		for (i = 0; i < count; i++) {
+			if (crc32c_async_submit(a, blocks[i / per_block] + (size_t)(i % per_block) * stride, size, 0,
+						bench_done, &slots[i]))
+				return 2;
+			if (i % 64 == 63 && crc32c_async_flush(a))
+				return 2;
+		}
+		if (crc32c_async_drain(a))
+			return 2;
+		if (p == 0)
+			for (i = 0; i < count; i++)
+				bad += slots[i].err || slots[i].got != slots[i].want;
+	}
+	t1 = now_s();
+	printf("{\"payload_bytes\": %u, \"payloads\": %u, \"passes\": %u, \"zerocopy\": %u, \"bad\": %u, "
+	       "\"GiBps\": %.3f, \"payloads_per_s\": %.0f}\n",
+	       size, count, passes, zerocopy, bad, (double)size * count * passes / (t1 - t0) / (1u << 30),
+	       (double)count * passes / (t1 - t0));
+	crc32c_async_destroy(a);
+	for (i = 0; i < nblocks; i++)
+		crc32c_pages_free(blocks[i], 11);
+	crc32c_pages_trim();
+	return bad ? 1 : 0;
+}
+
 int main(int argc, char **argv)
 {
 	static const unsigned int sizes[] = {0, 1, 100, 4096, 4097, 65536, 131072, 1 << 20, (4 << 20) + 3,
@@ -89,6 +171,9 @@ int main(int argc, char **argv)
 	unsigned int i, k, c;
 	int ep, rc, ndev = 1;
 
+	if (argc > 5 && !strcmp(argv[1], "bench"))
+		return bench_main((unsigned int)atoi(argv[2]), (unsigned int)atoi(argv[3]), (unsigned int)atoi(argv[4]),
+				  (unsigned int)atoi(argv[5]));
 	if (nctx < 1 || nctx > 16)
 		return 2;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
