@@ -10,9 +10,10 @@
 //              place over the host link) -- and records one descriptor per
 //              piece.  A payload larger than what a slot has left is cut
 //              into pieces; piece 0 carries the seed, later pieces seed 0.
-//   flush()    H2D of the packed staging runs and the descriptors, plan +
-//              main kernels, D2H of the results, an event, and a host
-//              function that bumps the eventfd.
+//   flush()    H2D of the packed staging runs, plan + main kernels (the plan
+//              reads the descriptors in place from pinned memory), D2H of the
+//              results, and a host function that marks the slot finished and
+//              bumps the eventfd -- four stream operations per batch.
 //   complete() harvests finished slots in launch order, folds each piece
 //              into its payload (crc <- crc32c_combine(crc, piece, len)),
 //              frees the slot, and runs the callbacks of finished payloads
@@ -27,6 +28,7 @@
 #include <sys/eventfd.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <deque>
 #include <map>
 #include <mutex>
@@ -187,8 +189,10 @@ struct Slot {
 	void *d_ws = nullptr;
 	uint8_t *h_stage = nullptr, *d_stage = nullptr;
 	pech_desc *h_desc = nullptr, *d_desc = nullptr;
+	const pech_desc *desc_view = nullptr; // device mapping of h_desc: the plan kernel reads it in place
 	uint32_t *h_out = nullptr, *d_out = nullptr;
-	hipEvent_t done = nullptr;
+	std::atomic<int> finished{0}; // set by the stream's host function after the results' D2H
+	int efd = -1;                 // the context's eventfd
 	std::vector<Piece> pieces;
 	std::vector<std::pair<size_t, size_t>> packed; // staging runs filled by memcpy: [lo, hi)
 	size_t used = 0;
@@ -240,12 +244,11 @@ static void slot_free(Slot *s)
 		(void)hipHostFree(s->h_out);
 	if (s->d_out)
 		(void)hipFree(s->d_out);
-	if (s->done)
-		(void)hipEventDestroy(s->done);
+
 	delete s;
 }
 
-static Slot *slot_new(void)
+static Slot *slot_new(int efd)
 {
 	Slot *s = new Slot();
 	if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -255,21 +258,28 @@ static Slot *slot_new(void)
 	    hipHostMalloc(&s->h_desc, kSlotDescs * sizeof(pech_desc), hipHostMallocDefault) != hipSuccess ||
 	    hipMalloc(&s->d_desc, kSlotDescs * sizeof(pech_desc)) != hipSuccess ||
 	    hipHostMalloc(&s->h_out, kSlotDescs * 4u, hipHostMallocDefault) != hipSuccess ||
-	    hipMalloc(&s->d_out, kSlotDescs * 4u) != hipSuccess ||
-	    hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess) {
+	    hipMalloc(&s->d_out, kSlotDescs * 4u) != hipSuccess) {
 		pech_internal_set_err("crc32c_async: slot allocation failed: %s", hipGetErrorString(hipGetLastError()));
 		slot_free(s);
 		return nullptr;
 	}
 	s->pieces.reserve(kSlotDescs);
+	s->efd = efd;
+	void *dv = nullptr;
+	if (hipHostGetDevicePointer(&dv, s->h_desc, 0) == hipSuccess && dv)
+		s->desc_view = (const pech_desc *)dv;
+	else
+		(void)hipGetLastError(); // no mapping: descriptors go by H2D copy
 	return s;
 }
 
 static void host_notify(void *arg)
 {
-	// HIP runtime thread: only the eventfd is touched here
+	// HIP runtime thread: only the slot's flag and the eventfd are touched
+	Slot *s = (Slot *)arg;
+	s->finished.store(1, std::memory_order_release);
 	const uint64_t one = 1;
-	ssize_t r = write(*(int *)arg, &one, sizeof(one));
+	ssize_t r = write(s->efd, &one, sizeof(one));
 	(void)r;
 }
 
@@ -298,9 +308,15 @@ static int reap(crc32c_async *a, bool wait_oldest)
 {
 	while (!a->inflight.empty()) {
 		Slot *s = a->inflight.front();
-		hipError_t q = wait_oldest ? hipEventSynchronize(s->done) : hipEventQuery(s->done);
-		if (q == hipErrorNotReady)
+		hipError_t q = hipSuccess;
+		if (wait_oldest) {
+			q = hipStreamSynchronize(s->stream);
+			while (q == hipSuccess && !s->finished.load(std::memory_order_acquire)) {
+				// the host function runs on the runtime's thread: a moment
+			}
+		} else if (!s->finished.load(std::memory_order_acquire)) {
 			return 0;
+		}
 		int err = 0;
 		if (q != hipSuccess) {
 			pech_internal_set_err("crc32c_async: batch failed: %s", hipGetErrorString(q));
@@ -327,7 +343,7 @@ static int get_slot(crc32c_async *a, Slot **out)
 			return 0;
 		}
 	if (a->slots.size() < kMaxSlots) {
-		Slot *s = slot_new();
+		Slot *s = slot_new(a->efd);
 		if (!s)
 			return -ENOMEM;
 		a->slots.push_back(s);
@@ -352,13 +368,18 @@ static int launch_slot(crc32c_async *a)
 		TRY_HIP(hipMemcpyAsync(s->d_stage + r.first, s->h_stage + r.first, r.second - r.first,
 				       hipMemcpyHostToDevice, s->stream),
 			-EIO);
-	TRY_HIP(hipMemcpyAsync(s->d_desc, s->h_desc, m * sizeof(pech_desc), hipMemcpyHostToDevice, s->stream), -EIO);
-	int rc = pech_internal_launch(s->d_desc, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream);
+	const pech_desc *descs = s->desc_view;
+	if (!descs) {
+		TRY_HIP(hipMemcpyAsync(s->d_desc, s->h_desc, m * sizeof(pech_desc), hipMemcpyHostToDevice, s->stream),
+			-EIO);
+		descs = s->d_desc;
+	}
+	s->finished.store(0, std::memory_order_relaxed);
+	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream);
 	if (rc)
 		return rc;
 	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), -EIO);
-	TRY_HIP(hipEventRecord(s->done, s->stream), -EIO);
-	TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, &a->efd), -EIO);
+	TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), -EIO);
 	s->inflight = true;
 	a->inflight.push_back(s);
 	a->cur = nullptr;
@@ -414,8 +435,10 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 	const uint8_t *p = (const uint8_t *)buf;
 	size_t left = len;
 	uint32_t placed = 0;
-	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len ? pinned_dev_addr(buf, len) : 0;
-	const bool dma = !zc && len && crc32c_pages_is_pinned(buf, len);
+	// one registry lookup: pinned pages are read in place (zero-copy) or DMA'd
+	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
+	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) ? dv : 0;
+	const bool dma = !zc && dv != 0;
 	do {
 		Slot *s = nullptr;
 		int rc = get_slot(a, &s);
