@@ -299,7 +299,7 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan_c
 // ---- main kernel ----------------------------------------------------------
 #ifdef PECH_STAMPS // diagnostic build: per-wave entry/start/end s_memrealtime stamps
 #define PECH_MAX_STAMPS 8192u
-#define PECH_NSTAMP 8u // start, end, tag, entry, scan, find, plan, fill
+#define PECH_NSTAMP 12u // start, end, tag, entry, scan, find, plan, fill, 25/50/75% of the first step, spare
 __device__ uint64_t pech_stamps[PECH_NSTAMP * PECH_MAX_STAMPS];
 #define STAMP(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
 extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
@@ -786,6 +786,10 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifdef PECH_PRIO_YOUNG // diagnostic: younger waves (higher age rank on the SIMD) issue first
 	set_prio(wave >> 2);
 #endif
+#ifdef PECH_STAMPS
+	uint64_t tq[3] = {0, 0, 0};
+	uint32_t nstep = 0;
+#endif
 	while (S.T) {
 		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 		if (STEP_ZOFF(S))
@@ -796,6 +800,10 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// full blocks: every lane's rows valid, prefetch stays inside every run
 		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
 			const uint64_t base = S.ad + (uint64_t)blk * U * PECH_ROW_BYTES;
+#ifdef PECH_STAMPS
+			if (nstep == 0 && (blk == nblk / 4u || blk == nblk / 2u || blk == 3u * nblk / 4u))
+				tq[blk == nblk / 4u ? 0 : (blk == nblk / 2u ? 1 : 2)] = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef PECH_PRIO_ROTATE // diagnostic: rotate issue priority among the SIMD's waves every block
 			set_prio((blk + (wave >> 2)) & 3u);
 #endif
@@ -839,6 +847,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		}
 		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));
 		S = N;
+#ifdef PECH_STAMPS
+		++nstep;
+#endif
 	}
 #ifdef PECH_STAMPS
 	const uint32_t wid = blockIdx.x * PECH_MAIN_WAVES + wave;
@@ -854,6 +865,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		st[5] = t_find;
 		st[6] = t_plan;
 		st[7] = t_fill;
+		st[8] = tq[0];
+		st[9] = tq[1];
+		st[10] = tq[2];
 	}
 #endif
 }

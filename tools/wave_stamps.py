@@ -23,17 +23,19 @@ torch.cuda.synchronize()
 L = _lib.lib()
 L.pech_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 W = 4096
-NS = 8
+NS = 12
 st = np.zeros(NS * W, dtype=np.uint64)
 assert L.pech_read_stamps(st.ctypes.data, W) == 0
-s, e, tag, ent, tscan, tfind, tplan, tfill = (st[k::NS].astype(np.int64) for k in range(NS))
+s, e, tag, ent, tscan, tfind, tplan, tfill, q1, q2, q3, _ = (st[k::NS].astype(np.int64) for k in range(NS))
 ok = (s > 0) & (e > 0)
 s, e, tag, ent = s[ok], e[ok], tag[ok], ent[ok]
 tscan, tfind, tplan, tfill = tscan[ok], tfind[ok], tplan[ok], tfill[ok]
+q1, q2, q3 = q1[ok], q2[ok], q3[ok]
 xcc, blk = tag & 0xF, tag >> 8
 # s_memrealtime: 100 MHz chip-wide clock (10 ns ticks)
 t0 = ent.min()
 s -= t0; e -= t0; ent -= t0; tscan -= t0; tfind -= t0; tplan -= t0; tfill -= t0
+q1 -= t0; q2 -= t0; q3 -= t0
 pro = s - ent
 span = e.max()
 pct = lambda a, q: float(np.percentile(a, q))
@@ -68,6 +70,21 @@ wid = np.nonzero(ok)[0]
 slot = wid % wpg
 print("end p50 by wave slot (us):", [round(pct(e[slot == k], 50) / 100, 1) for k in range(wpg)])
 print("busy p50 by wave slot (us):", [round(pct((e - s)[slot == k], 50) / 100, 1) for k in range(wpg)])
+# bytes-over-time profile: each wave's rows are piecewise linear between its
+# start, 25/50/75% stamps (first step; c3 waves have one) and end
+if cfg == "c3" and (q1 > 0).all():
+    per_wave = int(sizes.sum()) / len(s)
+    bins = np.arange(0, int(e.max()) + 500, 500)  # 5 us
+    prog = np.zeros(len(bins))
+    for k, (a, b) in enumerate(((s, q1), (q1, q2), (q2, q3), (q3, e))):
+        for i in range(len(s)):
+            lo, hi = a[i], b[i]
+            if hi <= lo:
+                continue
+            ov = np.clip(np.minimum(bins[1:], hi) - np.maximum(bins[:-1], lo), 0, None)
+            prog[:-1] += ov / (hi - lo) * per_wave / 4
+    rate = prog[:-1] / 5e-6 / 1e9
+    print("HBM read rate by 5 us bin (GB/s):", [int(x) for x in rate])
 out_dir = os.path.join(REPO, "gpurun_out")
 os.makedirs(out_dir, exist_ok=True)
 np.savez(os.path.join(out_dir, f"stamps_{cfg}.npz"), start=s, end=e, entry=ent, tag=tag, wid=wid)
