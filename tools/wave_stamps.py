@@ -52,6 +52,7 @@ print("mean wave busy / span: %.3f" % float(((e - s) / span).mean()))
 hist, edges = np.histogram(e / 100, bins=12)
 print("end-time histogram (us):", [(round(float(edges[i]),1), int(hist[i])) for i in range(len(hist))])
 
+print("workgroups on XCC blockIdx %% 8: %.3f" % float(((blk % 8) == xcc).mean()))
 for x in range(8):
     m = xcc == x
     print(f"xcc{x}: waves {int(m.sum())} end p10 {pct(e[m],10)/100:.1f} p50 {pct(e[m],50)/100:.1f} max {e[m].max()/100:.1f} us")
