@@ -649,10 +649,20 @@ __device__ __forceinline__ void finish_run(const uint32_t *lds, uint32_t g8, uin
 	lo = (g8 & 4u) ? o : u;
 	hi = (g8 & 4u) ? u : o;
 	u = adv_tab(lds, L_TAB64, lo) ^ hi;
-	if (active && g8 == 0) {
-		if (m)
-			u = shift_bytes(lds + L_POWB / 4u, m, u);
-		atomicXor(out + orig, u);
+	uint32_t v = 0;
+	if (active && g8 == 0)
+		v = m ? shift_bytes(lds + L_POWB / 4u, m, u) : u;
+	// A split step (every active group on one buffer) folds its 8 group
+	// results in registers: one atomic per wave instead of 8 on one address.
+	const uint32_t o0 = uni(orig);
+	if (__ballot(active && orig != o0) == 0ull) {
+		v ^= __shfl_xor(v, 8);
+		v ^= __shfl_xor(v, 16);
+		v ^= __shfl_xor(v, 32);
+		if ((threadIdx.x & 63u) == 0)
+			atomicXor(out + o0, v);
+	} else if (active && g8 == 0) {
+		atomicXor(out + orig, v);
 	}
 }
 
@@ -931,6 +941,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.8 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.9 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }
