@@ -699,11 +699,15 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// loads below, and the LDS fill is done before the scan's barriers --
 	// issued after the ring prime they would queue behind its HBM loads
 	// (vmcnt is in order; measured 4 us of prologue).
-	static_assert(PECH_MAIN_THREADS == 1024u, "table fill: one A_128 word per thread");
+	static_assert(1024u % PECH_MAIN_THREADS == 0u, "table fill: A_128 words split evenly over the threads");
+	constexpr uint32_t T128 = 1024u / PECH_MAIN_THREADS; // A_128 words per thread
 	constexpr uint32_t NT4 = (PECH_C_TAB1 - PECH_C_TAB4) / 4u; // single-copy tables, 16-B words
 	constexpr uint32_t TPT = (NT4 + PECH_MAIN_THREADS - 1u) / PECH_MAIN_THREADS;
 	const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
-	const uint32_t t128 = consts[PECH_C_TAB128 + tid];
+	uint32_t t128[T128];
+#pragma unroll
+	for (uint32_t j = 0; j < T128; ++j)
+		t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
 	u32x4 tv[TPT];
 #pragma unroll
 	for (uint32_t k = 0; k < TPT; ++k)
@@ -724,13 +728,14 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// A_128 once per bank: its 32 copies as 8 x 16 B; lane t starts at
 		// copy group t mod 8 so neighbouring lanes, whose rows are 256 B
 		// apart, write different banks.  Then the single-copy tables.
-		{
-			const uint32_t k = tid >> 8, e = tid & 0xFFu;
-			const u32x4 v = (u32x4)(t128);
+#pragma unroll
+		for (uint32_t j = 0; j < T128; ++j) {
+			const uint32_t w = tid + j * PECH_MAIN_THREADS, k = w >> 8, e = w & 0xFFu;
+			const u32x4 v = (u32x4)(t128[j]);
 			char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
 #pragma unroll
 			for (uint32_t q = 0; q < 8u; ++q)
-				*(u32x4 *)(dst + 16u * ((q + tid) & 7u)) = v;
+				*(u32x4 *)(dst + 16u * ((q + w) & 7u)) = v;
 		}
 #pragma unroll
 		for (uint32_t k = 0; k < TPT; ++k)
