@@ -52,15 +52,25 @@ struct crc32c_desc {
 #define CRC32C_F_HOST 0u   /* bufs are pageable host memory                */
 #define CRC32C_F_DEVICE 1u /* bufs are device memory on the current device */
 #define CRC32C_F_PINNED 2u /* bufs are pinned host memory (read in place)   */
+#define CRC32C_F_ALL_DEVICES 4u /* with CRC32C_F_PINNED: shard over every GPU */
 
 /*
  * out[i] = crc32c(seeds ? seeds[i] : 0, bufs[i], lens[i]) for i < n.
  * Synchronous.  Pageable host buffers are moved with hipMemcpyAsync through
- * pinned staging (double-buffered, overlapped with the kernel); pinned
- * buffers (CRC32C_F_PINNED: hipHostMalloc'd or registered) are read by the
- * kernel in place through their device mapping (zero-copy), falling back to
- * DMA staging if a buffer has none.  Results come back with one D2H copy per
- * sub-batch.
+ * pinned staging (double-buffered, one copy stream per slot, overlapped with
+ * the kernel).  Pinned buffers (CRC32C_F_PINNED: hipHostMalloc'd, registered
+ * or crc32c_pages memory) of 1 MiB or more are DMA'd straight from their
+ * pages; smaller ones are read by the kernel in place through their device
+ * mapping (zero-copy: no host memcpy, no per-buffer DMA call), falling back
+ * to staging if a buffer has no mapping.  Results come back with one D2H
+ * copy per sub-batch.
+ * CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES: the batch is split into contiguous,
+ * byte-balanced shards, one per visible GPU, each read in place over its own
+ * host link; all shards are issued from the calling thread before any is
+ * waited for (pech's one thread drives a whole node).  Every
+ * buffer must be mapped on every GPU (hipHostMalloc / crc32c_pages memory);
+ * otherwise -EINVAL and nothing is launched.  Other flag combinations with
+ * CRC32C_F_ALL_DEVICES are -EINVAL.
  */
 int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
 		 uint32_t *out, unsigned int n, unsigned int flags);

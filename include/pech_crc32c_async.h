@@ -71,8 +71,11 @@ typedef void (*crc32c_done_fn)(void *arg, uint32_t crc, int err);
 
 /* flags for crc32c_async_create() */
 #define CRC32C_ASYNC_DEFAULT 0u
-/* payloads in crc32c_pages memory are read by the kernel in place over the
- * host link (no H2D copy); without it they are DMA'd to device slots */
+/* payloads in crc32c_pages memory below 1 MiB are read by the kernel in
+ * place over the host link (no H2D copy, no per-payload DMA call); larger
+ * ones are still DMA'd to device slots, which moves big payloads faster
+ * (MI355X: 50 vs 37 GiB/s at 4 MiB).  Without the flag every payload is
+ * DMA'd. */
 #define CRC32C_ASYNC_ZEROCOPY 1u
 
 /* A context on the current device: its own HIP stream, staging slots and

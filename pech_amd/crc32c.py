@@ -19,7 +19,7 @@ __all__ = [
     "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc",
 ]
 
-F_HOST, F_DEVICE, F_PINNED = 0, 1, 2
+F_HOST, F_DEVICE, F_PINNED, F_ALL_DEVICES = 0, 1, 2, 4
 
 
 def crc32c(crc, data):

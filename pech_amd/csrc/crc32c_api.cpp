@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -89,7 +90,7 @@ struct DevCtx {
 	void *d_ws = nullptr;
 	size_t ws_bytes = 0;
 	// synchronous host paths
-	hipStream_t s_comp = nullptr, s_copy = nullptr;
+	hipStream_t s_comp = nullptr, s_copy[2] = {nullptr, nullptr}; // one copy stream per staging slot
 	uint8_t *h_stage[2] = {nullptr, nullptr};
 	uint8_t *d_stage[2] = {nullptr, nullptr};
 	size_t stage_bytes = 0;
@@ -140,7 +141,8 @@ static int ctx_get(DevCtx **out)
 		HIP_TRY(hipMalloc(&c->d_consts, PECH_C_WORDS * sizeof(uint32_t)));
 		HIP_TRY(hipMemcpy(c->d_consts, host_consts(), PECH_C_WORDS * sizeof(uint32_t), hipMemcpyHostToDevice));
 		HIP_TRY(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
-		HIP_TRY(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking));
+		for (int i = 0; i < 2; ++i) // two slots' copies may run on two DMA engines at once
+			HIP_TRY(hipStreamCreateWithFlags(&c->s_copy[i], hipStreamNonBlocking));
 		for (int i = 0; i < 2; ++i) {
 			HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
 			HIP_TRY(hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
@@ -280,7 +282,7 @@ static int stage_reserve(DevCtx *c, size_t bytes, uint32_t ndesc)
 
 static const size_t STAGE_BYTES = 64u << 20;      // per slot
 static const uint32_t STAGE_DESCS = 1u << 16;     // per slot
-static const size_t PINNED_DIRECT_MIN = 64u << 10; // pinned buffers >= this are DMA'd in place
+static const size_t PINNED_DIRECT_MIN = 1u << 20; // pinned buffers >= this are DMA'd, smaller ones read in place
 
 // One sub-batch of host buffers into slot `s`: gather bytes, enqueue copy,
 // kernels and result copy.  Buffers must each fit the slot.
@@ -294,11 +296,23 @@ static int enqueue_host_slot(DevCtx *c, int s, const void *const *bufs, const un
 		const unsigned int i = i0 + k;
 		const size_t len = lens[i];
 		const bool direct = (flags & CRC32C_F_PINNED) && len >= PINNED_DIRECT_MIN;
+		void *zc = nullptr; // small pinned buffer: the kernel reads it in place (no host memcpy)
+		if ((flags & CRC32C_F_PINNED) && !direct && len &&
+		    (hipHostGetDevicePointer(&zc, const_cast<void *>(bufs[i]), 0) != hipSuccess || !zc)) {
+			(void)hipGetLastError();
+			zc = nullptr;
+		}
+		if (zc) {
+			c->h_desc[s][k].addr = (uint64_t)(uintptr_t)zc;
+			c->h_desc[s][k].len = (uint32_t)len;
+			c->h_desc[s][k].seed = chain_seed ? *chain_seed : (seeds ? seeds[i] : 0u);
+			continue;
+		}
 		if (direct) {
 			if (off > packed_lo)
 				HIP_TRY(hipMemcpyAsync(c->d_stage[s] + packed_lo, c->h_stage[s] + packed_lo,
-						       off - packed_lo, hipMemcpyHostToDevice, c->s_copy));
-			HIP_TRY(hipMemcpyAsync(c->d_stage[s] + off, bufs[i], len, hipMemcpyHostToDevice, c->s_copy));
+						       off - packed_lo, hipMemcpyHostToDevice, c->s_copy[s]));
+			HIP_TRY(hipMemcpyAsync(c->d_stage[s] + off, bufs[i], len, hipMemcpyHostToDevice, c->s_copy[s]));
 		} else if (len) {
 			memcpy(c->h_stage[s] + off, bufs[i], len);
 		}
@@ -311,10 +325,10 @@ static int enqueue_host_slot(DevCtx *c, int s, const void *const *bufs, const un
 	}
 	if (off > packed_lo)
 		HIP_TRY(hipMemcpyAsync(c->d_stage[s] + packed_lo, c->h_stage[s] + packed_lo, off - packed_lo,
-				       hipMemcpyHostToDevice, c->s_copy));
+				       hipMemcpyHostToDevice, c->s_copy[s]));
 	HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)m * sizeof(pech_desc), hipMemcpyHostToDevice,
-			       c->s_copy));
-	HIP_TRY(hipEventRecord(c->ev_copied[s], c->s_copy));
+			       c->s_copy[s]));
+	HIP_TRY(hipEventRecord(c->ev_copied[s], c->s_copy[s]));
 	HIP_TRY(hipStreamWaitEvent(c->s_comp, c->ev_copied[s], 0));
 	int rc = ws_reserve(c, m);
 	if (rc)
@@ -349,50 +363,138 @@ static int host_big(DevCtx *c, const void *buf, size_t len, uint32_t seed, uint3
 	return 0;
 }
 
-// Pinned host buffers read in place by the kernel over the host link
-// (zero-copy: hipHostMalloc'd / registered memory is mapped into the GPU's
-// address space).  Measured faster than DMA staging on MI355X boxes (bench
-// msgr_async).  Returns 1 if some buffer has no device mapping (caller
-// falls back to DMA staging).
-static int pinned_zero_copy(DevCtx *c, const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
-			    uint32_t *out, unsigned int n)
+// CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES: contiguous byte-balanced shards,
+// one per device (PECH_DEVICES="0,0,..." overrides the list; at most two
+// shards per device, on its two slots -- how the 1-GPU tests split a batch).
+// Every shard's sub-batch is enqueued before any is waited for, so the GPUs
+// read their host links concurrently from this one thread.
+static int multi_device_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
+			       uint32_t *out, unsigned int n)
 {
-	int rc = stage_reserve(c, c->stage_bytes ? c->stage_bytes : STAGE_BYTES, STAGE_DESCS);
-	if (rc)
-		return rc;
-	for (unsigned int i0 = 0; i0 < n; i0 += STAGE_DESCS) {
-		const unsigned int m = (n - i0) < STAGE_DESCS ? (n - i0) : STAGE_DESCS;
-		for (unsigned int k = 0; k < m; ++k) {
+	int devs[64], nd = 0;
+	if (const char *e = getenv("PECH_DEVICES")) {
+		for (const char *p = e; *p && nd < 64;) {
+			char *q = nullptr;
+			const long v = strtol(p, &q, 10);
+			if (q == p)
+				break;
+			devs[nd++] = (int)v;
+			p = *q == ',' ? q + 1 : q;
+		}
+	} else {
+		HIP_TRY(hipGetDeviceCount(&nd));
+		nd = nd < 64 ? nd : 64;
+		for (int d = 0; d < nd; ++d)
+			devs[d] = d;
+	}
+	int ndev_all = 0;
+	HIP_TRY(hipGetDeviceCount(&ndev_all));
+	int slot[64], used[64] = {0};
+	for (int k = 0; k < nd; ++k) {
+		if (devs[k] < 0 || devs[k] >= ndev_all || devs[k] >= 64 || used[devs[k]] >= 2) {
+			set_err("crc32c_batch: bad device list (PECH_DEVICES)");
+			return -EINVAL;
+		}
+		slot[k] = used[devs[k]]++;
+	}
+	if (nd == 0) {
+		set_err("no usable GPU");
+		return -ENODEV;
+	}
+	// shard k = buffers [cut[k], cut[k+1]): the first buffer whose byte prefix reaches k/nd of the total
+	std::vector<uint64_t> pre(n + 1, 0);
+	for (unsigned int i = 0; i < n; ++i)
+		pre[i + 1] = pre[i] + lens[i];
+	unsigned int cut[65];
+	for (int k = 0; k <= nd; ++k) {
+		const uint64_t target = (uint64_t)((__uint128_t)pre[n] * (unsigned)k / (unsigned)nd);
+		cut[k] = k == nd ? n : (unsigned int)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+	}
+	int cur = 0;
+	HIP_TRY(hipGetDevice(&cur));
+	struct Shard {
+		DevCtx *c;
+		unsigned int i0, m;
+	} sh[64];
+	int rc = 0;
+	// device mappings of every buffer on its shard's device first: no launch if one is missing
+	std::vector<uint64_t> dptr(n, 0);
+	for (int k = 0; k < nd && !rc; ++k) {
+		if ((rc = hipSetDevice(devs[k]) == hipSuccess ? 0 : -EIO))
+			break;
+		if ((rc = ctx_get(&sh[k].c)))
+			break;
+		if ((rc = stage_reserve(sh[k].c, sh[k].c->stage_bytes ? sh[k].c->stage_bytes : STAGE_BYTES, STAGE_DESCS)))
+			break;
+		if ((rc = ws_reserve(sh[k].c, STAGE_DESCS))) // before any launch: never regrown under one
+			break;
+		for (unsigned int i = cut[k]; i < cut[k + 1]; ++i) {
 			void *dp = nullptr;
-			const unsigned int i = i0 + k;
 			if (lens[i] && (hipHostGetDevicePointer(&dp, const_cast<void *>(bufs[i]), 0) != hipSuccess || !dp)) {
 				(void)hipGetLastError();
-				return i0 == 0 ? 1 : -EIO; // nothing launched yet: fall back
+				set_err("crc32c_batch: buffer %u is not mapped on device %d (CRC32C_F_ALL_DEVICES)", i, devs[k]);
+				rc = -EINVAL;
+				break;
 			}
-			c->h_desc[0][k].addr = (uint64_t)(uintptr_t)dp;
-			c->h_desc[0][k].len = lens[i];
-			c->h_desc[0][k].seed = seeds ? seeds[i] : 0u;
+			dptr[i] = (uint64_t)(uintptr_t)dp;
 		}
-		HIP_TRY(hipMemcpyAsync(c->d_desc[0], c->h_desc[0], (size_t)m * sizeof(pech_desc), hipMemcpyHostToDevice,
-				       c->s_comp));
-		if ((rc = ws_reserve(c, m)))
-			return rc;
-		if ((rc = launch_batch(c, c->d_desc[0], c->d_out[0], m, c->d_ws, c->ws_bytes, c->s_comp)))
-			return rc;
-		HIP_TRY(hipMemcpyAsync(c->h_out[0], c->d_out[0], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
-		HIP_TRY(hipStreamSynchronize(c->s_comp));
-		memcpy(out + i0, c->h_out[0], (size_t)m * 4u);
+		sh[k].i0 = cut[k];
 	}
-	return 0;
+	for (bool more = !rc; more && !rc;) {
+		more = false;
+		for (int k = 0; k < nd && !rc; ++k) { // enqueue one sub-batch per shard
+			Shard &S = sh[k];
+			S.m = cut[k + 1] - S.i0 < STAGE_DESCS ? cut[k + 1] - S.i0 : STAGE_DESCS;
+			if (!S.m)
+				continue;
+			DevCtx *c = S.c;
+			const int s = slot[k];
+			if ((rc = hipSetDevice(devs[k]) == hipSuccess ? 0 : -EIO))
+				break;
+			for (unsigned int j = 0; j < S.m; ++j) {
+				const unsigned int i = S.i0 + j;
+				c->h_desc[s][j].addr = dptr[i];
+				c->h_desc[s][j].len = lens[i];
+				c->h_desc[s][j].seed = seeds ? seeds[i] : 0u;
+			}
+			if (hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)S.m * sizeof(pech_desc), hipMemcpyHostToDevice,
+					   c->s_comp) != hipSuccess) {
+				set_err("hipMemcpyAsync: %s", hipGetErrorString(hipGetLastError()));
+				rc = -EIO;
+				break;
+			}
+			// two shards on one device share its stream (ordered), so one workspace serves both
+			if ((rc = launch_batch(c, c->d_desc[s], c->d_out[s], S.m, c->d_ws, c->ws_bytes, c->s_comp)))
+				break;
+			if (hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t)S.m * 4u, hipMemcpyDeviceToHost, c->s_comp) !=
+			    hipSuccess) {
+				set_err("hipMemcpyAsync: %s", hipGetErrorString(hipGetLastError()));
+				rc = -EIO;
+				break;
+			}
+		}
+		for (int k = 0; k < nd && !rc; ++k) { // then wait for them all
+			Shard &S = sh[k];
+			if (!S.m)
+				continue;
+			if (hipSetDevice(devs[k]) != hipSuccess || hipStreamSynchronize(S.c->s_comp) != hipSuccess) {
+				set_err("shard on device %d: %s", devs[k], hipGetErrorString(hipGetLastError()));
+				rc = -EIO;
+				break;
+			}
+			memcpy(out + S.i0, S.c->h_out[slot[k]], (size_t)S.m * 4u);
+			S.i0 += S.m;
+			more = more || S.i0 < cut[k + 1];
+		}
+	}
+	(void)hipSetDevice(cur);
+	return rc;
 }
 
 static int host_batch(DevCtx *c, const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
 		      uint32_t *out, unsigned int n, unsigned int flags)
 {
-	int rc;
-	if ((flags & CRC32C_F_PINNED) && (rc = pinned_zero_copy(c, bufs, lens, seeds, out, n)) <= 0)
-		return rc;
-	rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
+	int rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
 	if (rc)
 		return rc;
 	// slot bookkeeping for the double buffer
@@ -504,12 +606,15 @@ int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32
 {
 	if (n == 0)
 		return 0;
-	if (!bufs || !lens || !out || flags > (CRC32C_F_DEVICE | CRC32C_F_PINNED) ||
-	    ((flags & CRC32C_F_DEVICE) && (flags & CRC32C_F_PINNED))) {
+	if (!bufs || !lens || !out || flags > (CRC32C_F_DEVICE | CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES) ||
+	    ((flags & CRC32C_F_DEVICE) && (flags & CRC32C_F_PINNED)) ||
+	    ((flags & CRC32C_F_ALL_DEVICES) && !(flags & CRC32C_F_PINNED))) {
 		set_err("crc32c_batch: invalid arguments");
 		return -EINVAL;
 	}
 	std::lock_guard<std::mutex> lk(g_mu);
+	if (flags & CRC32C_F_ALL_DEVICES)
+		return multi_device_pinned(bufs, lens, seeds, out, n);
 	DevCtx *c = nullptr;
 	int rc = ctx_get(&c);
 	if (rc)

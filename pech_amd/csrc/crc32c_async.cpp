@@ -176,6 +176,7 @@ struct DeviceGuard {
 };
 
 constexpr size_t kSlotBytes = 32u << 20; // staging per slot
+constexpr size_t kZeroCopyMax = 1u << 20; // pinned payloads from this size up are DMA'd even in zero-copy mode
 constexpr uint32_t kSlotDescs = 8192;    // descriptors per slot
 constexpr unsigned kMaxSlots = 4;        // slots in flight per context
 
@@ -435,9 +436,10 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 	const uint8_t *p = (const uint8_t *)buf;
 	size_t left = len;
 	uint32_t placed = 0;
-	// one registry lookup: pinned pages are read in place (zero-copy) or DMA'd
+	// one registry lookup: pinned pages are read in place (zero-copy, below
+	// kZeroCopyMax) or DMA'd
 	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
-	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) ? dv : 0;
+	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len < kZeroCopyMax ? dv : 0;
 	const bool dma = !zc && dv != 0;
 	do {
 		Slot *s = nullptr;

@@ -72,6 +72,19 @@ def test_shift_combine_match_oracle():
     assert crc32c_combine(O.crc(9, a[:1234]), O.crc(0, a[1234:]), 5000 - 1234) == O.crc(9, a)
 
 
+def test_batch_flag_validation():
+    # checked before any device work: runs with or without a GPU
+    from pech_amd import _lib
+
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(b"abc")
+    p = (ctypes.c_void_p * 1)(ctypes.addressof(buf))
+    l = (ctypes.c_uint * 1)(3)
+    out = (ctypes.c_uint32 * 1)()
+    for flags in (3, 4, 5, 7, 8, 1 | 4):  # DEVICE|PINNED, ALL_DEVICES without PINNED, unknown bits
+        assert L.crc32c_batch(p, l, None, out, 1, flags) == -22, flags
+
+
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="checks the no-GPU failure mode")
 def test_no_gpu_fails_loudly():
     # without a GPU the batch API returns an error (no CPU fallback) ...

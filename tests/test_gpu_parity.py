@@ -268,6 +268,40 @@ def test_batch_host_pinned_device_flags(torch_dev, P):
     assert L.crc32c_batch(ptrs, cl, cs, out, n, 3) < 0
 
 
+@pytest.mark.parametrize("devices", [None, "0,0"])
+def test_batch_pinned_all_devices(torch_dev, P, monkeypatch, devices):
+    # CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES: byte-balanced shards, one per GPU,
+    # all issued before any wait.  "0,0" = two shards on GPU 0 (both slots,
+    # one stream): the split/gather path on a 1-GPU box.  Sub-batches of
+    # 65,536 descriptors: n > that takes several rounds per shard.
+    torch, dev = torch_dev
+    from pech_amd import _lib
+
+    if devices:
+        monkeypatch.setenv("PECH_DEVICES", devices)
+    rng = np.random.default_rng(12)
+    lens = np.concatenate([rng.integers(0, 5000, 140000), rng.integers(1 << 20, 3 << 20, 12), [0, 7, 4096]])
+    rng.shuffle(lens)
+    host = torch.empty(int(lens.sum()) + 64, dtype=torch.uint8).pin_memory()
+    data = rng.integers(0, 256, host.numel(), dtype=np.uint8)
+    host.copy_(torch.from_numpy(data))
+    offs = np.concatenate([[3], 3 + np.cumsum(lens)[:-1]])
+    seeds = rng.integers(0, 1 << 32, len(lens), dtype=np.uint64)
+    n = len(lens)
+    ptrs = (ctypes.c_void_p * n)(*[host.data_ptr() + int(o) for o in offs])
+    cl = (ctypes.c_uint * n)(*[int(x) for x in lens])
+    cs = (ctypes.c_uint32 * n)(*[int(x) for x in seeds])
+    out = (ctypes.c_uint32 * n)()
+    L = _lib.lib()
+    assert L.crc32c_batch(ptrs, cl, cs, out, n, P.F_PINNED | P.F_ALL_DEVICES) == 0, L.crc32c_last_error()
+    assert np.array_equal(np.frombuffer(out, dtype=np.uint32), O.crcs(data, offs, lens, seeds))
+    # pageable memory has no device mapping: refused before anything launches
+    page = np.zeros(1 << 16, np.uint8)
+    p1 = (ctypes.c_void_p * 1)(page.ctypes.data)
+    l1 = (ctypes.c_uint * 1)(1000)
+    assert L.crc32c_batch(p1, l1, None, out, 1, P.F_PINNED | P.F_ALL_DEVICES) == -22
+
+
 def test_concurrent_streams_explicit_workspaces(torch_dev, P):
     # bench.py's pipelined pass: independent batches alternate over streams,
     # one workspace per stream, launches overlapping on the device
