@@ -29,6 +29,8 @@ extern "C" hipError_t pech_launch_main(uint32_t, const pech_ws *, const uint32_t
 				       hipStream_t, hipEvent_t, hipEvent_t);
 
 extern "C" const char *pech_kernel_tag(void);
+extern "C" hipError_t pech_launch_small(const void *, uint32_t, uint32_t, const uint32_t *, uint32_t *, uint32_t,
+					hipStream_t);
 
 // ---------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -100,6 +102,10 @@ struct DevCtx {
 	uint32_t *d_out[2] = {nullptr, nullptr};
 	uint32_t desc_cap = 0;
 	hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+	// drop-in small path: device views of h_stage[0] and h_out[0] (zero-copy)
+	void *small_src = nullptr;
+	uint32_t *h_small = nullptr, *small_out = nullptr; // result + ticket, coherent pinned memory
+	uint32_t small_ticket = 0;
 	// timing
 	std::vector<TimedLaunch> pending;
 	std::vector<TimedLaunch> free_events;
@@ -141,6 +147,12 @@ static int ctx_get(DevCtx **out)
 		HIP_TRY(hipMalloc(&c->d_consts, PECH_C_WORDS * sizeof(uint32_t)));
 		HIP_TRY(hipMemcpy(c->d_consts, host_consts(), PECH_C_WORDS * sizeof(uint32_t), hipMemcpyHostToDevice));
 		HIP_TRY(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
+		{ // fine-grained: the small kernel's system-scope stores are visible while it runs
+			void *so = nullptr;
+			HIP_TRY(hipHostMalloc((void **)&c->h_small, 256, hipHostMallocCoherent | hipHostMallocMapped));
+			HIP_TRY(hipHostGetDevicePointer(&so, c->h_small, 0));
+			c->small_out = (uint32_t *)so;
+		}
 		for (int i = 0; i < 2; ++i) // two slots' copies may run on two DMA engines at once
 			HIP_TRY(hipStreamCreateWithFlags(&c->s_copy[i], hipStreamNonBlocking));
 		for (int i = 0; i < 2; ++i) {
@@ -252,6 +264,8 @@ static int stage_reserve(DevCtx *c, size_t bytes, uint32_t ndesc)
 			HIP_TRY(hipMalloc(&c->d_stage[i], bytes));
 		}
 		c->stage_bytes = bytes;
+		c->small_src = nullptr;
+		HIP_TRY(hipHostGetDevicePointer(&c->small_src, c->h_stage[0], 0));
 	}
 	if (ndesc > c->desc_cap) {
 		for (int i = 0; i < 2; ++i) {
@@ -589,9 +603,37 @@ uint32_t crc32c(uint32_t crc, const void *data, unsigned int length)
 		if (!rc)
 			rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
 		if (!rc) {
-			const void *b = data;
-			const uint32_t s = crc;
-			rc = host_batch(c, &b, &length, &s, &out, 1, CRC32C_F_HOST);
+			if (length <= PECH_SMALL_MAX) {
+				// one launch: bytes into pinned staging, read there in place
+				// The kernel writes the result, then this call's ticket, to
+				// pinned memory; polling the ticket saves the stream
+				// synchronisation (~3 us).  After ~20 ms of polling the
+				// stream is synchronised instead, which also reports errors.
+				memcpy(c->h_stage[0], data, length);
+				const uint32_t ticket = ++c->small_ticket ? c->small_ticket : ++c->small_ticket;
+				volatile uint32_t *res = (volatile uint32_t *)c->h_small;
+				if (pech_launch_small(c->small_src, length, crc, c->d_consts, c->small_out, ticket, c->s_comp) !=
+				    hipSuccess) {
+					set_err("small-buffer launch: %s", hipGetErrorString(hipGetLastError()));
+					rc = -EIO;
+				} else {
+					for (uint32_t spin = 0; res[1] != ticket && spin < (1u << 22); ++spin)
+						__builtin_ia32_pause();
+					if (res[1] != ticket && hipStreamSynchronize(c->s_comp) != hipSuccess) {
+						set_err("small-buffer kernel: %s", hipGetErrorString(hipGetLastError()));
+						rc = -EIO;
+					} else if (res[1] != ticket) {
+						set_err("small-buffer kernel finished without its result");
+						rc = -EIO;
+					} else {
+						out = res[0];
+					}
+				}
+			} else {
+				const void *b = data;
+				const uint32_t s = crc;
+				rc = host_batch(c, &b, &length, &s, &out, 1, CRC32C_F_HOST);
+			}
 		}
 	}
 	if (rc) {

@@ -296,6 +296,78 @@ extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan_c
 	plan_body<true>(descs, n, cores, lrs, partials, nzs, consts, out, dsts, deltas);
 }
 
+// ---- single small buffer (the drop-in crc32c()) ---------------------------
+// One workgroup, one launch: the buffer (<= PECH_SMALL_MAX bytes) is read in
+// place from pinned host staging (zero-copy: no DMA, no plan kernel), 16 B
+// per lane into LDS, then thread t runs the reference byte loop
+// (include/crc32c.h:92-93) over its contiguous segment, shifts its register
+// to the buffer end (x^(8m)) and the segments are XOR-reduced; the seed term
+// is x^(8 len) * seed.  The result goes straight to pinned host memory.
+#define PECH_SMALL_THREADS 1024u
+static_assert(PECH_SMALL_MAX % 16u == 0u, "small path: whole 16-byte loads");
+extern "C" __global__ __launch_bounds__(PECH_SMALL_THREADS) void pech_crc32c_small(
+	const uint8_t *__restrict__ src, uint32_t len, uint32_t seed, const uint32_t *__restrict__ consts,
+	uint32_t *__restrict__ out, uint32_t ticket)
+{
+	__shared__ __attribute__((aligned(16))) uint8_t data[PECH_SMALL_MAX];
+	__shared__ uint32_t t1[256];
+	__shared__ uint32_t powb[384];
+	__shared__ uint32_t red[PECH_SMALL_THREADS / 64u];
+	const uint32_t tid = threadIdx.x;
+	if (tid < 256u)
+		t1[tid] = consts[PECH_C_TAB1 + tid];
+	if (tid < 384u)
+		powb[tid] = consts[PECH_C_POWB + tid];
+	// the staging buffer is 16-byte aligned and at least PECH_SMALL_MAX long:
+	// whole 16-byte loads past len stay inside it and are never used
+	constexpr uint32_t LPT = PECH_SMALL_MAX / 16u / PECH_SMALL_THREADS; // loads per thread, all in flight at once
+	u32x4 w[LPT];
+#pragma unroll
+	for (uint32_t k = 0; k < LPT; ++k) {
+		const uint32_t i = tid + k * PECH_SMALL_THREADS;
+		if (i * 16u < len)
+			w[k] = *(const g_u32x4 *)(src + 16u * i);
+	}
+#pragma unroll
+	for (uint32_t k = 0; k < LPT; ++k) {
+		const uint32_t i = tid + k * PECH_SMALL_THREADS;
+		if (i * 16u < len)
+			*(u32x4 *)(data + 16u * i) = w[k];
+	}
+	__syncthreads();
+	// segments of whole 16-byte words, read as such (byte reads at a stride
+	// of the segment length hit the same LDS banks from every lane)
+	const uint32_t seg = ((len + PECH_SMALL_THREADS - 1u) / PECH_SMALL_THREADS + 15u) & ~15u;
+	const uint32_t b0 = min(len, tid * seg), b1 = min(len, b0 + seg);
+	uint32_t c = 0;
+	for (uint32_t j = b0; j < b1; j += 16u) {
+		const u32x4 q = *(const u32x4 *)(data + j);
+		const uint32_t e = min(16u, b1 - j);
+#pragma unroll
+		for (uint32_t k = 0; k < 16u; ++k) {
+			const uint32_t byte = (q[k >> 2] >> (8u * (k & 3u))) & 0xFFu;
+			if (k < e)
+				c = t1[(c ^ byte) & 0xFFu] ^ (c >> 8);
+		}
+	}
+	uint32_t v = (b1 > b0 && len > b1) ? shift_bytes(powb, len - b1, c) : c;
+	for (uint32_t d = 1; d < 64; d <<= 1)
+		v ^= __shfl_xor(v, d);
+	if ((tid & 63u) == 0)
+		red[tid >> 6] = v;
+	__syncthreads();
+	if (tid == 0) {
+		uint32_t r = seed ? shift_bytes(powb, len, seed) : 0u;
+		for (uint32_t w = 0; w < PECH_SMALL_THREADS / 64u; ++w)
+			r ^= red[w];
+		// result, then the caller's ticket: the host polls out[1] (system scope)
+		__builtin_nontemporal_store(r, out);
+		__threadfence_system();
+		__builtin_nontemporal_store(ticket, out + 1);
+		__threadfence_system();
+	}
+}
+
 // ---- main kernel ----------------------------------------------------------
 #ifdef PECH_STAMPS // diagnostic build: per-wave entry/start/end s_memrealtime stamps
 #define PECH_MAX_STAMPS 8192u
@@ -908,6 +980,16 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 }
 
 // ---- host-side launchers (used by crc32c_api.cpp) -------------------------
+extern "C" hipError_t pech_launch_small(const void *src, uint32_t len, uint32_t seed, const uint32_t *consts,
+					uint32_t *out, uint32_t ticket, hipStream_t stream)
+{
+	if (len > PECH_SMALL_MAX)
+		return hipErrorInvalidValue;
+	hipLaunchKernelGGL(pech_crc32c_small, dim3(1), dim3(PECH_SMALL_THREADS), 0, stream, (const uint8_t *)src, len,
+			   seed, consts, out, ticket);
+	return hipGetLastError();
+}
+
 // dsts != NULL: the fused-copy variant (destination address per descriptor)
 extern "C" hipError_t pech_launch_plan(const pech_desc *descs, uint32_t n, const pech_ws *ws, const uint32_t *consts,
 				       uint32_t *out, const uint64_t *dsts, hipStream_t stream)

@@ -35,6 +35,7 @@
 #define PECH_RPW_MIN 64u          /* min rows per wave (8 KiB)             */
 #define PECH_LARGE_ROWS 2048u     /* size-class cap for the plan's ordering  */
 #define PECH_SPLIT_ROWS 256u      /* >= this: a buffer is split over 8 groups */
+#define PECH_SMALL_MAX 65536u     /* drop-in crc32c(): one-launch path up to this */
 
 /* constants block (u32 words), built on the host, uploaded once per device */
 #define PECH_C_TAB128 0u    /* A_128 byte tables, 4 x 256  (row Horner step)  */

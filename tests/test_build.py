@@ -39,7 +39,7 @@ def kernel_body(asm, name):
 
 
 @pytest.mark.parametrize("kernel", ["pech_crc32c_plan", "pech_crc32c_main", "pech_crc32c_plan_copy",
-                                    "pech_crc32c_main_copy"])
+                                    "pech_crc32c_main_copy", "pech_crc32c_small"])
 def test_no_calls_no_scratch(device_asm, kernel):
     asm, _ = device_asm
     body = kernel_body(asm, kernel)

@@ -231,6 +231,19 @@ def test_dropin_crc32c_host_memory(P):
     assert P.crc32c(0x1234, b"") == 0x1234
 
 
+def test_dropin_small_path_boundaries(P):
+    # crc32c() up to PECH_SMALL_MAX (64 KiB) is one zero-copy launch; above
+    # it the staged batch path.  Sizes around both paths' edges, unaligned
+    # sources, random seeds
+    rng = np.random.default_rng(18)
+    big = rng.integers(0, 256, (1 << 17) + 64, dtype=np.uint8)
+    for n in (1, 2, 15, 16, 17, 63, 64, 65, 1023, 1024, 1025, 4097, 65535, 65536, 65537, 70001):
+        for off in (0, 1, 13):
+            d = big[off:off + n].tobytes()
+            s = int(rng.integers(0, 1 << 32))
+            assert P.crc32c(s, d) == O.crc(s, d), (n, off)
+
+
 def test_dropin_crc32c_larger_than_staging(P):
     # > 64 MiB staging slot: chained through the seed inside the library
     d = np.random.default_rng(9).integers(0, 256, (64 << 20) + 4097, dtype=np.uint8)
