@@ -231,6 +231,7 @@ def main():
                              "avg_launch_us": round(float(psamp.mean()), 2) if len(psamp) else None}
     if rank == 0 and world == 1 and not args.no_host_path and not dsts:
         line["pcie_inclusive"] = host_path(args, bufs[0], offs, sizes, outs, P)
+        line["dropin_crc32c"] = dropin_latency(P)
         # uniform payloads: the C adapter benchmark (no Python per submit);
         # mixed batches through ctypes, where payloads are few enough for the
         # Python loop not to be the bound
@@ -300,6 +301,29 @@ def host_path(args, buf0, offs, sizes, outs, P):
                                   "unit": "GiB/s", "path": "crc32c_batch(CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES) "
                                   "from one host thread", "matches_device_path": True}
     return res
+
+
+def dropin_latency(P):
+    """Per-call latency of the drop-in crc32c() (pageable host memory, one
+    synchronous call per buffer, as messenger.c calls it per header and per
+    <=4 KiB piece).  Each size's result is checked against crc32c_batch on
+    the same bytes (the staged batch path)."""
+    from pech_amd import _lib
+
+    lib = _lib.lib()
+    res = {}
+    for n in (49, 4096, 65536):
+        buf = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
+        p = buf.ctypes.data
+        if lib.crc32c(0, p, n) != P.crc32c_batch([buf.tobytes()])[0]:
+            raise SystemExit("PARITY FAILURE: drop-in crc32c() differs from crc32c_batch")
+        t = []
+        for _ in range(300):
+            t0 = time.perf_counter()
+            lib.crc32c(0, p, n)
+            t.append(time.perf_counter() - t0)
+        res[str(n)] = round(float(np.median(t)) * 1e6, 2)
+    return {"p50_us_by_bytes": res, "path": "crc32c(0, buf, n) from pageable memory, synchronous"}
 
 
 def msgr_path(args, buf0, offs, sizes, outs, P):
