@@ -150,6 +150,7 @@ static int ctx_get(DevCtx **out)
 		{ // fine-grained: the small kernel's system-scope stores are visible while it runs
 			void *so = nullptr;
 			HIP_TRY(hipHostMalloc((void **)&c->h_small, 256, hipHostMallocCoherent | hipHostMallocMapped));
+			memset(c->h_small, 0, 256); // ticket 0 is never issued
 			HIP_TRY(hipHostGetDevicePointer(&so, c->h_small, 0));
 			c->small_out = (uint32_t *)so;
 		}
