@@ -78,6 +78,10 @@ int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32
 /*
  * Device batch, asynchronous on `stream` (a hipStream_t, NULL = default
  * stream): d_out[i] = crc32c(d_descs[i].seed, d_descs[i].addr, d_descs[i].len).
+ * The lengths of one call must total below 512 GiB (the kernels count 128-byte
+ * rows in 32 bits); more than HBM holds, so only descriptors aliasing the same
+ * memory can reach it -- split such batches (the synchronous crc32c_batch
+ * does this itself).
  * d_descs and d_out are device memory of the current device; the call only
  * enqueues work (no host synchronisation, no allocation once the internal
  * workspace is large enough: see crc32c_dev_reserve()).  Buffers and

@@ -378,6 +378,18 @@ static int host_big(DevCtx *c, const void *buf, size_t len, uint32_t seed, uint3
 	return 0;
 }
 
+// Descriptors [i0, i0 + m) of one launch: at most STAGE_DESCS, and at most
+// PECH_LAUNCH_MAX_BYTES of payload (the kernels count a launch's rows in
+// 32 bits; only descriptors aliasing the same memory could exceed it).
+static unsigned int launch_take(const unsigned int *lens, unsigned int i0, unsigned int end)
+{
+	uint64_t bytes = 0;
+	unsigned int m = 0;
+	while (i0 + m < end && m < STAGE_DESCS && (m == 0 || bytes + lens[i0 + m] <= PECH_LAUNCH_MAX_BYTES))
+		bytes += lens[i0 + m++];
+	return m;
+}
+
 // CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES: contiguous byte-balanced shards,
 // one per device (PECH_DEVICES="0,0,..." overrides the list; at most two
 // shards per device, on its two slots -- how the 1-GPU tests split a batch).
@@ -459,7 +471,7 @@ static int multi_device_pinned(const void *const *bufs, const unsigned int *lens
 		more = false;
 		for (int k = 0; k < nd && !rc; ++k) { // enqueue one sub-batch per shard
 			Shard &S = sh[k];
-			S.m = cut[k + 1] - S.i0 < STAGE_DESCS ? cut[k + 1] - S.i0 : STAGE_DESCS;
+			S.m = launch_take(lens, S.i0, cut[k + 1]);
 			if (!S.m)
 				continue;
 			DevCtx *c = S.c;
@@ -567,8 +579,8 @@ static int device_batch_sync(DevCtx *c, const void *const *bufs, const unsigned 
 	int rc = stage_reserve(c, c->stage_bytes ? c->stage_bytes : STAGE_BYTES, STAGE_DESCS);
 	if (rc)
 		return rc;
-	for (unsigned int i0 = 0; i0 < n; i0 += STAGE_DESCS) {
-		const unsigned int m = (n - i0) < STAGE_DESCS ? (n - i0) : STAGE_DESCS;
+	for (unsigned int i0 = 0, m; i0 < n; i0 += m) {
+		m = launch_take(lens, i0, n);
 		for (unsigned int k = 0; k < m; ++k) {
 			c->h_desc[0][k].addr = (uint64_t)(uintptr_t)bufs[i0 + k];
 			c->h_desc[0][k].len = lens[i0 + k];

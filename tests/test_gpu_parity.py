@@ -315,6 +315,27 @@ def test_batch_pinned_all_devices(torch_dev, P, monkeypatch, devices):
     assert L.crc32c_batch(p1, l1, None, out, 1, P.F_PINNED | P.F_ALL_DEVICES) == -22
 
 
+def test_batch_device_aliasing_beyond_launch_limit(torch_dev, P):
+    # 60,000 descriptors over ONE 5 MiB device buffer: 293 GiB of payload,
+    # past the 256 GiB per-launch cap (rows are counted in 32 bits), so
+    # crc32c_batch splits it into two launches
+    torch, dev = torch_dev
+    from pech_amd import _lib
+
+    rng = np.random.default_rng(14)
+    L5 = 5 << 20
+    host = rng.integers(0, 256, L5, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    n = 60000
+    ptrs = (ctypes.c_void_p * n)(*([d.data_ptr()] * n))
+    lens = (ctypes.c_uint * n)(*([L5] * n))
+    out = (ctypes.c_uint32 * n)()
+    L = _lib.lib()
+    assert L.crc32c_batch(ptrs, lens, None, out, n, P.F_DEVICE) == 0, L.crc32c_last_error()
+    got = np.frombuffer(out, dtype=np.uint32)
+    assert np.all(got == O.crc(0, host))
+
+
 def test_concurrent_streams_explicit_workspaces(torch_dev, P):
     # bench.py's pipelined pass: independent batches alternate over streams,
     # one workspace per stream, launches overlapping on the device
