@@ -9,7 +9,7 @@ HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h pech_amd/csrc/api_internal.h in
 LIB = pech_amd/libpech_crc32c.so
 OBJ = build/crc32c_kernels.o build/crc32c_api.o build/crc32c_async.o
 
-all: $(LIB) oracle build/msgr_sim
+all: $(LIB) oracle build/msgr_sim build/dropin_kat
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -44,6 +44,12 @@ build/msgr_sim: tests/c/msgr_sim.c oracle/crc32c_oracle.c include/pech_crc32c_as
 	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
 		tests/c/msgr_sim.c oracle/crc32c_oracle.c -Lpech_amd -lpech_crc32c -L/opt/rocm/lib -lamdhip64 \
 		-Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
+
+# test program: the drop-in crc32c() from C, as messenger.c calls it
+build/dropin_kat: tests/c/dropin_kat.c include/crc32c.h $(LIB)
+	@mkdir -p build
+	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude tests/c/dropin_kat.c -Lpech_amd -lpech_crc32c \
+		-L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
 
 oracle:
 	$(MAKE) -C oracle all

@@ -107,3 +107,50 @@ def test_no_gpu_fails_loudly():
     r2 = subprocess.run([sys.executable, "-c", code2], cwd=REPO, capture_output=True, timeout=120)
     assert r2.returncode != 0
     assert b"crc32c() failed" in r2.stderr
+
+
+def _xorshift_bytes(n):
+    # SURVEY Appendix A's generator (tests/c/dropin_kat.c gen())
+    out = np.empty(n, np.uint8)
+    s = 0x2545F491
+    for i in range(n):
+        s ^= (s << 13) & 0xFFFFFFFF
+        s ^= s >> 17
+        s ^= (s << 5) & 0xFFFFFFFF
+        out[i] = s & 0xFF
+    return out
+
+
+def test_dropin_kat_builds_as_pech_c():
+    r = subprocess.run(["make", "-s", "-C", REPO, "build/dropin_kat"], capture_output=True)
+    assert r.returncode == 0, r.stderr.decode()
+
+
+@pytest.mark.gpu
+def test_dropin_from_c_matches_appendix_a():
+    # the drop-in called from gnu89 C (one call, the <=4 KiB page-piece chain
+    # of ceph_crc32c_iov, a 49-byte header call) against the golden vectors
+    # the compiled reference produced (tests/golden/kat.json)
+    import json
+
+    kat = json.load(open(os.path.join(REPO, "tests", "golden", "kat.json")))
+    exe = os.path.join(REPO, "build", "dropin_kat")
+    assert os.path.exists(exe), "build/dropin_kat is built by `make` (__graft_entry__.build())"
+    args, want = [], {}
+    for e in kat["appendix_a"]:
+        for seed_hex, crc in e["crc"].items():
+            args.append("%d:%s" % (e["len"], seed_hex))
+            want[(e["len"], int(seed_hex, 16))] = crc
+    r = subprocess.run([exe] + args, capture_output=True, timeout=300)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    fields = r.stdout.decode().split()
+    rows = [fields[i:i + 5] for i in range(0, len(fields), 5)]
+    assert len(rows) == len(args)
+    hdr_want = {}
+    for n, seed, whole, pieces, hdr in rows:
+        n, seed = int(n), int(seed, 16)
+        assert int(whole, 16) == want[(n, seed)], (n, seed)
+        assert int(pieces, 16) == want[(n, seed)], (n, seed)
+        if n not in hdr_want:
+            hdr_want[n] = O.crc(0, _xorshift_bytes(min(n, 49)))
+        assert int(hdr, 16) == hdr_want[n], n
