@@ -15,8 +15,14 @@ Multi-GPU: batches are independent, so each rank checksums its own shard
 (weak scaling); no collective touches the data path -- the only
 communication is the timing barrier and a MAX all-reduce of the elapsed time.
 
+Two timed passes of K steps each, both bracketed by barrier + synchronize:
+a one-stream pass (batches back to back; `serial`, and the roofline), then
+the `value` pass with consecutive batches alternating over two streams (own
+workspace each), so one batch's plan kernel, launch boundaries, prologue and
+tail overlap its neighbour's streaming -- how a server drives the library.
+
 Prints ONE JSON line (rank 0).  `roofline` is for the main kernel: HIP
-events around every main-kernel launch on the stream it runs on give the
+events around every main-kernel launch of the one-stream pass give the
 average launch duration; achieved = algorithmic bytes per launch (sum of
 buffer lengths) / that duration, against 8.0 TB/s HBM3E peak
 (/opt/skills/guides/MI355X_MICROARCH.md).  `cpu_baseline` times the
@@ -71,10 +77,9 @@ def parse():
     ap.add_argument("--host-passes", type=int, default=4)
     ap.add_argument("--op", default="crc", choices=["crc", "copy"],
                     help="crc: the checksum path; copy: fused CRC + copy to a second buffer (SURVEY 8f row 4)")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="HIP streams that consecutive batches alternate over (own workspace each)")
-    ap.add_argument("--pipeline-streams", type=int, default=2,
-                    help="second timed pass with batches alternating over this many streams (0: skip)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams that consecutive batches alternate over (own workspace each) in the timed "
+                         "pass that gives `value`; a one-stream pass always gives the per-launch roofline")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
     ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
@@ -123,7 +128,7 @@ def main():
             d = torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
             dsts.append((d, torch.from_numpy((d.data_ptr() + offs).astype(np.int64)).to(dev)))
     assert _lib.lib().crc32c_dev_reserve(n) == 0
-    maxs = max(1, args.streams, args.pipeline_streams)
+    maxs = max(1, args.streams)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(maxs - 1)]
     wsb = P.workspace_bytes(n)
     wss = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(maxs)]
@@ -168,8 +173,15 @@ def main():
             elapsed = float(t.item())
         return elapsed, samples
 
+    # Pass 1, one stream: batches back to back; its per-launch main-kernel
+    # durations (dispatch-packet events, non-overlapping) give the roofline.
+    # Pass 2, `--streams` streams (default 2): consecutive batches alternate
+    # over them, so one batch's plan kernel, launch boundaries, prologue and
+    # tail overlap its neighbour's streaming -- how a server runs the library
+    # (the async layer keeps four batches in flight).  Pass 2 is `value`.
     nstreams = max(1, args.streams)
-    elapsed, samples = timed(nstreams, args.steps, args.warmup)
+    serial_el, samples = timed(1, args.steps, args.warmup)
+    elapsed = serial_el if nstreams == 1 else timed(nstreams, args.steps, args.warmup)[0]
     launches = len(samples)
     kernel_ms = float(samples.sum()) / 1e3
 
@@ -216,19 +228,10 @@ def main():
                      "bytes_per_launch": algo_bytes, "avg_launch_us": round(avg_kernel_s * 1e6, 2),
                      "launch_us_p10_p50_p90": [round(float(np.percentile(samples, q)), 2) for q in (10, 50, 90)]
                      if len(samples) else None,
-                     "launches": launches},
+                     "launches": launches, "pass": "one stream (serial), K launches"},
+        "serial": {"streams": 1, "value": round(total_bytes / serial_el / (1 << 30), 2), "unit": "GiB/s",
+                   "ms_per_step": round(serial_el / args.steps * 1e3, 4)},
     }
-
-    if args.pipeline_streams > 1 and args.pipeline_streams != nstreams:
-        # Same batches, consecutive ones on alternating streams: one batch's
-        # plan kernel, launch boundary, prologue and tail overlap its
-        # neighbour's streaming.  Reported beside `value` (per-launch
-        # durations overlap here, so the roofline comes from the serial pass).
-        pel, psamp = timed(args.pipeline_streams, args.steps, args.warmup)
-        line["pipelined"] = {"streams": args.pipeline_streams,
-                             "value": round(total_bytes / pel / (1 << 30), 2), "unit": "GiB/s",
-                             "ms_per_step": round(pel / args.steps * 1e3, 4),
-                             "avg_launch_us": round(float(psamp.mean()), 2) if len(psamp) else None}
     if rank == 0 and world == 1 and not args.no_host_path and not dsts:
         line["pcie_inclusive"] = host_path(args, bufs[0], offs, sizes, outs, P)
         line["dropin_crc32c"] = dropin_latency(P)

@@ -11,7 +11,7 @@ stop() { echo "stopping after rc=$1 ($2)"; exit "$1"; }
 TAG=$(python3 -c "import sys; sys.path.insert(0,'.'); import pech_amd as P; print(P.version())")
 for C in ${CFGS:-c3}; do
   CFG=${C%-copy}; OP=crc; [ "$C" != "$CFG" ] && OP=copy
-  BENCH="bench.py --no-cpu-baseline --no-host-path --pipeline-streams 0 --config $CFG --op $OP"
+  BENCH="bench.py --no-cpu-baseline --no-host-path --streams 1 --config $CFG --op $OP"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${C}_trace -o run \
     -- python3 $BENCH --steps 20 > gpurun_out/prof_${C}_trace.log 2>&1 || stop $? "trace $C"
   tail -1 gpurun_out/prof_${C}_trace.log

@@ -19,6 +19,7 @@ for cfg in ${STAMP_CONFIGS:-}; do
     || stop $? "stamps $cfg"
   grep -v "amdgpu.ids\|^xcc\|histogram" gpurun_out/stamps_$cfg.txt
 done
+# columns: value (2-stream pass) GiB/s, main GB/s, roofline frac, main us, serial (1-stream) GiB/s
 # AB_ENVS: space-separated variants, each a comma-separated VAR=value list ("-" = none)
 for ev in ${AB_ENVS:--}; do
 for lib in ${AB_LIBS:-pech_amd/libpech_crc32c.so}; do
@@ -27,7 +28,7 @@ for lib in ${AB_LIBS:-pech_amd/libpech_crc32c.so}; do
     envs=""; [ "$ev" != - ] && envs=${ev//,/ }
     env $envs PECH_CRC32C_LIB=$lib timeout -k 10 240 python bench.py --config $cfg --steps 30 --no-cpu-baseline --no-host-path \
       ${AB_EXTRA:-} > $o 2>&1 || { tail -5 $o; stop $? "bench $lib $cfg"; }
-    echo "$(basename $lib) $ev $cfg: $(tail -1 $o | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["achieved"], r["frac"], r["avg_launch_us"], d.get("pipelined", {}).get("value"))')"
+    echo "$(basename $lib) $ev $cfg: $(tail -1 $o | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["achieved"], r["frac"], r["avg_launch_us"], d.get("serial", {}).get("value"))')"
   done
 done
 done
