@@ -94,11 +94,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # PECH_BENCH_BACKEND=gloo rehearses the N>1 bench on a box with fewer
+    # GPUs than ranks (ranks share devices round-robin; timing all-reduce on
+    # the host).  The driver's N>1 runs use the default: RCCL, one GPU per rank.
+    backend = os.environ.get("PECH_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -168,7 +177,7 @@ def main():
         samples = np.asarray(P.timing_samples(), dtype=np.float64) * 1e3  # us per main-kernel launch
         P.timing(False)
         if dist is not None:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         return elapsed, samples
