@@ -11,9 +11,34 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(REPO, "oracle", "liboracle_crc32c.so")
 REF_SO = os.path.join(REPO, "oracle", "_ref", "libref_crc32c.so")
+HW_SO = os.path.join(REPO, "oracle", "liboracle_hw.so")
 
 _o = None
 _r = None
+_h = None
+
+
+def hw():
+    """SSE4.2 CRC32C (oracle/crc32c_hw.c): a CPU context baseline, or None
+    when the library is absent or this host lacks SSE4.2."""
+    global _h
+    if _h is None:
+        try:
+            flags = open("/proc/cpuinfo").read()
+        except OSError:
+            flags = ""
+        if " sse4_2" not in flags:
+            return None
+        if not os.path.exists(HW_SO):
+            subprocess.check_call(["make", "-C", os.path.join(REPO, "oracle"), "all"])
+        L = ctypes.CDLL(HW_SO)
+        L.hw_crc32c.restype = ctypes.c_uint32
+        L.hw_crc32c.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint]
+        L.hw_crc32c_batch_mt.restype = ctypes.c_int
+        L.hw_crc32c_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]
+        _h = L
+    return _h
 
 
 def oracle():

@@ -99,3 +99,32 @@ def test_algebra_shift_combine():
         d = a.copy()
         d[:4] ^= np.frombuffer(np.uint32(s).tobytes(), dtype=np.uint8)
         assert O.crc(0, d) == O.crc(s, a)
+
+
+def test_sse42_context_baseline_matches_oracle():
+    """bench.py's SSE4.2 CPU row (oracle/crc32c_hw.c) is bit-exact with the
+    reference loop: golden vectors, then random lengths around its 3-stream
+    threshold at every alignment, random seeds, and the threaded batch."""
+    H = O.hw()
+    if H is None:
+        pytest.skip("no SSE4.2 on this host")
+    for row in KAT["appendix_a"]:
+        if row["len"] > 65536:
+            continue
+        d = np.frombuffer(bytes(xorshift_bytes(row["len"])), dtype=np.uint8).copy()
+        for s, want in row["crc"].items():
+            assert H.hw_crc32c(int(s, 16), d.ctypes.data, d.nbytes) == want, (row["len"], s)
+    rng = np.random.default_rng(7)
+    buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    for _ in range(400):
+        n = int(rng.choice([rng.integers(0, 64), rng.integers(1000, 1100), rng.integers(0, 200000)]))
+        off = int(rng.integers(0, 16))
+        seed = int(rng.integers(0, 1 << 32))
+        assert H.hw_crc32c(seed, buf.ctypes.data + off, n) == O.crc(seed, buf[off:off + n]), (n, off)
+    lens = rng.integers(0, 70000, 300).astype(np.uint32)
+    offs = np.cumsum(np.concatenate([[3], lens[:-1].astype(np.uint64) + 5])).astype(np.uint64)
+    big = rng.integers(0, 256, int(offs[-1] + lens[-1] + 8), dtype=np.uint8)
+    out = np.zeros(len(lens), dtype=np.uint32)
+    assert H.hw_crc32c_batch_mt(big.ctypes.data, offs.ctypes.data, lens.ctypes.data, out.ctypes.data, len(lens), 4,
+                                2) == 0
+    assert np.array_equal(out, O.crcs(big, offs, lens))
