@@ -136,6 +136,43 @@ __global__ __launch_bounds__(1024) void k_group(const uint8_t *p, uint32_t rows_
 		out[gid] = x;
 }
 
+// k_group<8, D, nt> restricted to the workgroups that land on the XCCs in
+// `xmask` (HW_REG_XCC_ID; the others exit at once): per-XCD read bandwidth
+// with the rest of the chip idle
+template <int D>
+__global__ __launch_bounds__(1024) void k_group_xcc(const uint8_t *p, uint32_t rows_per_group, uint32_t *out,
+						    uint32_t xmask)
+{
+	uint32_t xcc;
+	asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+	if (!((xmask >> (xcc & 7u)) & 1u))
+		return;
+	const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) / 8;
+	const uint32_t gl = threadIdx.x % 8;
+	const uint8_t *base = p + (size_t)gid * rows_per_group * 128 + gl * 16;
+	u32x4 acc = (u32x4)(0u);
+	u32x4 ring[D];
+#pragma unroll
+	for (int d = 0; d < D; ++d)
+		ring[d] = ldp<true>(base + (size_t)d * 128);
+	uint32_t r = D;
+	for (; r + D <= rows_per_group; r += D) {
+#pragma unroll
+		for (int d = 0; d < D; ++d) {
+			acc ^= ring[d];
+			ring[d] = ldp<true>(base + (size_t)(r + d) * 128);
+		}
+	}
+#pragma unroll
+	for (int d = 0; d < D; ++d)
+		acc ^= ring[d];
+	for (; r < rows_per_group; ++r)
+		acc ^= ldp<true>(base + (size_t)r * 128);
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[gid] = x;
+}
+
 static float time_it(void (*launch)(void *), void *arg, int reps)
 {
 	hipEvent_t a, b;
@@ -232,6 +269,32 @@ int main(int argc, char **argv)
 		const float ms = time_it(probes[i].fn, &a, reps);
 		printf("  {\"probe\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}%s\n", probes[i].name, ms * 1e3,
 		       a.bytes / (ms * 1e-3) / 1e9, i + 1 < sizeof(probes) / sizeof(probes[0]) ? "," : "");
+	}
+	printf("]");
+	// per-XCD rates: only the workgroups on the XCCs of each mask read
+	// (bytes read = bytes x popcount(mask) / 8: workgroups are placed on
+	// XCCs round-robin, 32 per XCC)
+	const uint32_t masks[] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x55, 0xAA, 0x0F, 0xF0, 0xFF};
+	printf(",\n\"per_xcd\": [\n");
+	for (size_t i = 0; i < sizeof(masks) / sizeof(masks[0]); ++i) {
+		const uint32_t rpg = (uint32_t)(a.bytes / 128 / ((size_t)a.ncu * 128));
+		hipEvent_t e0, e1;
+		CHECK(hipEventCreate(&e0));
+		CHECK(hipEventCreate(&e1));
+		hipLaunchKernelGGL((k_group_xcc<8>), dim3(a.ncu), dim3(1024), 0, 0, a.buf[0], rpg, a.out, masks[i]);
+		CHECK(hipDeviceSynchronize());
+		CHECK(hipEventRecord(e0));
+		for (int r = 0; r < reps; ++r)
+			hipLaunchKernelGGL((k_group_xcc<8>), dim3(a.ncu), dim3(1024), 0, 0, a.buf[r & 1], rpg, a.out,
+					   masks[i]);
+		CHECK(hipEventRecord(e1));
+		CHECK(hipEventSynchronize(e1));
+		float ms;
+		CHECK(hipEventElapsedTime(&ms, e0, e1));
+		ms /= reps;
+		const double rd = (double)a.bytes * __builtin_popcount(masks[i]) / 8.0;
+		printf("  {\"xcc_mask\": \"0x%02x\", \"us\": %.2f, \"GBps\": %.1f}%s\n", masks[i], ms * 1e3,
+		       rd / (ms * 1e-3) / 1e9, i + 1 < sizeof(masks) / sizeof(masks[0]) ? "," : "");
 	}
 	printf("]}\n");
 	return 0;
