@@ -25,8 +25,10 @@ def device_asm():
         pytest.skip("hipcc not available")
     d = tempfile.mkdtemp()
     out = os.path.join(d, "k.s")
+    # PECH_TEST_KFLAGS: extra -D flags, to hold an A/B variant to the same ISA checks
+    extra = os.environ.get("PECH_TEST_KFLAGS", "").split()
     r = subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                        "-Rpass-analysis=kernel-resource-usage", SRC, "-o", out],
+                        "-Rpass-analysis=kernel-resource-usage", *extra, SRC, "-o", out],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     return open(out).read(), r.stderr
