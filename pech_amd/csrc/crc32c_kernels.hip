@@ -61,6 +61,14 @@
 #endif
 
 
+// Split-step results are XORed into a workgroup table in LDS and reach out[]
+// with one global atomic per (workgroup, buffer), issued by the workgroup's
+// last wave to finish: the
+// waves of a 4 MiB buffer (16 per workgroup, 64 in a 256 MiB launch) then no
+// longer queue on one address (measured: 4 MiB class 52.0 -> 50.0 us).
+#define PECH_DEFER_SLOTS 64u
+#define PECH_DEFER_EMPTY 0xFFFFFFFFu
+
 // ---- LDS map of the main kernel (bytes) ---------------------------------
 #define L_REP 0u                 // 128 KiB: A_128, 32 bank copies
 #define L_TAB4 131072u           // 4 KiB each, single copy
@@ -71,7 +79,10 @@
 #define L_CHUNK (L_POWB + 1536u) // 4 KiB: chunk row offsets
 #define L_NZ (L_CHUNK + 4096u)   // 4 KiB: chunk non-empty counts
 #define L_MISC (L_NZ + 4096u)    // scan scratch
-#define L_BYTES (L_MISC + 128u)
+#define L_DEFER (L_MISC + 128u)  // 512 B: split-step results, keyed by output slot
+#define L_DEFER_DONE (L_DEFER + 8u * PECH_DEFER_SLOTS) // waves of the workgroup done
+#define L_BYTES (L_DEFER_DONE + 16u)
+static_assert(L_BYTES <= 160u * 1024u, "main kernel LDS over 160 KiB");
 
 static_assert(L_POWB - L_TAB4 == 4u * (PECH_C_POWB - PECH_C_TAB4), "LDS/consts layout mismatch");
 static_assert(L_BYTES <= 160u * 1024u, "LDS budget");
@@ -701,7 +712,7 @@ __device__ __forceinline__ void horner_row_pred(const uint32_t *lds, uint32_t lr
 // Fold a group's 32 stream registers into the CRC of its run (as a message
 // ending at the run's last row), shift it to the buffer's core end plus the
 // tail (m bytes), xor into out[orig].
-__device__ __forceinline__ void finish_run(const uint32_t *lds, uint32_t g8, uint32_t s0, uint32_t s1, uint32_t s2,
+__device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t s0, uint32_t s1, uint32_t s2,
 					   uint32_t s3, uint64_t m, bool active, uint32_t *out, uint32_t orig)
 {
 	uint32_t u = adv_tab(lds, L_TAB4, s0) ^ s1;
@@ -731,8 +742,17 @@ __device__ __forceinline__ void finish_run(const uint32_t *lds, uint32_t g8, uin
 		v ^= __shfl_xor(v, 8);
 		v ^= __shfl_xor(v, 16);
 		v ^= __shfl_xor(v, 32);
-		if ((threadIdx.x & 63u) == 0)
-			atomicXor(out + o0, v);
+		if ((threadIdx.x & 63u) == 0) {
+			// the workgroup's table: slot o0 % 64, claimed by CAS; a slot
+			// held by another buffer falls back to the global atomic
+			uint32_t *keys = (uint32_t *)lds + L_DEFER / 4u, *vals = keys + PECH_DEFER_SLOTS;
+			const uint32_t sl = o0 & (PECH_DEFER_SLOTS - 1u);
+			const uint32_t prev = atomicCAS(keys + sl, PECH_DEFER_EMPTY, o0);
+			if (prev == PECH_DEFER_EMPTY || prev == o0)
+				atomicXor(vals + sl, v);
+			else
+				atomicXor(out + o0, v);
+		}
 	} else if (active && g8 == 0) {
 		atomicXor(out + orig, v);
 	}
@@ -813,6 +833,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		for (uint32_t k = 0; k < TPT; ++k)
 			if (tid + k * PECH_MAIN_THREADS < NT4)
 				*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
+		if (tid < PECH_DEFER_SLOTS) { // empty deferral table (published by the scan's barriers)
+			lds[L_DEFER / 4u + tid] = PECH_DEFER_EMPTY;
+			lds[L_DEFER / 4u + PECH_DEFER_SLOTS + tid] = 0u;
+			if (tid == 0)
+				lds[L_DEFER_DONE / 4u] = 0u;
+		}
 #pragma unroll
 		for (uint32_t k = 0; k < CPT; ++k) {
 			const uint32_t c = tid * CPT + k;
@@ -938,6 +964,24 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		++nstep;
 #endif
 	}
+	// The workgroup's last wave to finish flushes the deferred split-step
+	// results (no barrier: the others exit).  A wave's LDS operations complete
+	// in order and the fences keep the compiler from moving them, so every
+	// earlier wave's table updates precede its count.
+	{
+		uint32_t done = 0;
+		__threadfence_block(); // table updates before the count (compiler and LDS order)
+		if (lane == 0)
+			done = atomicAdd(lds + L_DEFER_DONE / 4u, 1u);
+		done = uni(__shfl(done, 0));
+		__threadfence_block();
+		static_assert(PECH_DEFER_SLOTS == 64u, "one slot per lane of the flushing wave");
+		if (done == PECH_MAIN_WAVES - 1u) {
+			const uint32_t k = lds[L_DEFER / 4u + lane];
+			if (k != PECH_DEFER_EMPTY)
+				atomicXor(out + k, lds[L_DEFER / 4u + PECH_DEFER_SLOTS + lane]);
+		}
+	}
 #ifdef PECH_STAMPS
 	const uint32_t wid = blockIdx.x * PECH_MAIN_WAVES + wave;
 	if (lane == 0 && wid < PECH_MAX_STAMPS) {
@@ -1028,6 +1072,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.9 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.10 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }
