@@ -3,13 +3,15 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
-SRC = pech_amd/csrc/crc32c_kernels.hip pech_amd/csrc/crc32c_api.cpp pech_amd/csrc/crc32c_async.cpp
+SRC = pech_amd/csrc/crc32c_kernels.hip pech_amd/csrc/crc32c_api.cpp pech_amd/csrc/crc32c_async.cpp \
+      pech_amd/csrc/crc32c_cpu.c
+CFLAGS_HOST ?= -O2 -std=gnu11 -fPIC -Wall -Wextra -Werror
 HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h pech_amd/csrc/api_internal.h include/crc32c.h include/pech_crc32c.h \
       include/pech_crc32c_async.h
 LIB = pech_amd/libpech_crc32c.so
-OBJ = build/crc32c_kernels.o build/crc32c_api.o build/crc32c_async.o
+OBJ = build/crc32c_kernels.o build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
 
-all: $(LIB) oracle build/msgr_sim build/dropin_kat
+all: $(LIB) oracle build/msgr_sim build/dropin_kat build/coro_stack
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -23,6 +25,11 @@ build/crc32c_async.o: pech_amd/csrc/crc32c_async.cpp $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
+# host routine + library stack: plain C, no HIP (never includes oracle/)
+build/crc32c_cpu.o: pech_amd/csrc/crc32c_cpu.c pech_amd/csrc/gf2.h
+	@mkdir -p build
+	gcc $(CFLAGS_HOST) -c $< -o $@
+
 $(LIB): $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
 
@@ -33,9 +40,10 @@ asm: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 		../pech_amd/csrc/crc32c_kernels.hip -o crc32c_kernels.s
 
 # A/B diagnostic build: make variant V=name D="-DPECH_U=9" -> build/lib_name.so
-variant: build/crc32c_api.o build/crc32c_async.o
+variant: build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
 	$(HIPCC) $(HIPFLAGS) $(D) -c pech_amd/csrc/crc32c_kernels.hip -o build/k_$(V).o
-	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o build/crc32c_api.o build/crc32c_async.o
+	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o build/crc32c_api.o build/crc32c_async.o \
+		build/crc32c_cpu.o
 
 # test program: pech's receive path on the async layer (gnu89, epoll loop);
 # links the test oracle for the expected footer CRCs -- not product code
@@ -50,6 +58,13 @@ build/dropin_kat: tests/c/dropin_kat.c include/crc32c.h $(LIB)
 	@mkdir -p build
 	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude tests/c/dropin_kat.c -Lpech_amd -lpech_crc32c \
 		-L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
+
+# test program: the library from a 64 KiB pech-style coroutine stack
+# (pech itself needs -D_FORTIFY_SOURCE=0 for its cross-stack longjmp)
+build/coro_stack: tests/c/coro_stack.c oracle/crc32c_oracle.c include/pech_crc32c_async.h $(LIB)
+	@mkdir -p build
+	gcc -std=gnu89 -O2 -Wall -Werror -U_FORTIFY_SOURCE -D_FORTIFY_SOURCE=0 -Iinclude tests/c/coro_stack.c oracle/crc32c_oracle.c -Lpech_amd \
+		-lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
 
 oracle:
 	$(MAKE) -C oracle all

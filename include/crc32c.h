@@ -14,10 +14,15 @@
  * length 0 returns `crc`; any alignment; `data` is read only.  Chaining holds
  * exactly: crc32c(crc32c(s, A, |A|), B, |B|) == crc32c(s, A||B, |A|+|B|).
  *
- * `data` is HOST memory.  The bytes are staged to the GPU and checksummed by
- * the gfx950 kernel; the call is synchronous and cannot fail (a HIP failure
- * aborts the process with a message -- the library has no CPU fallback).
- * For throughput use the batch API in pech_crc32c.h.
+ * `data` is HOST memory.  The call is synchronous and, like the reference,
+ * cannot fail.  Calls of up to crc32c_set_cpu_max() bytes (default 4 MiB:
+ * every header, front/middle section and <=4 KiB data piece the messenger
+ * hashes) run on the host (SSE4.2 crc32, 3 streams,
+ * ~0.01 us for a 49-byte header); larger ones are staged to the GPU and
+ * checksummed by the gfx950 kernel, on a library-owned stack (safe from
+ * pech's 64 KiB coroutine stacks, src/sched.c:16).  If the GPU path fails
+ * the bytes are recomputed on the host (crc32c_get_stats() counts it).
+ * Throughput belongs to the batch / async APIs (pech_crc32c*.h).
  */
 #ifndef _CRC32C_H
 #define _CRC32C_H

@@ -24,10 +24,14 @@
  * Conventions (pech style, include/err.h): int-returning calls give 0 or a
  * negative errno: -EINVAL bad arguments, -ENOMEM allocation failure, -EIO a
  * HIP failure (crc32c_last_error() has the text), -ENODEV no usable GPU.
- * There is no CPU fallback: without a GPU every compute call fails loudly.
- * Threading: one caller thread at a time per process (pech is one OS thread,
- * README:11-16); HIP calls need more than pech's 64 KiB coroutine stacks
- * (src/sched.c:16) -- see INTEGRATION.md.
+ * Batch, device and async calls never fall back to the CPU: without a GPU
+ * they fail loudly.  Only the drop-in crc32c() (crc32c.h) stays total.
+ * Threading: any thread may call; pech uses one (README:11-16).  Every entry
+ * point that calls HIP runs on a per-thread 8 MiB library stack, so pech's
+ * 64 KiB coroutine stacks (src/sched.c:16) need no change.
+ * The internal workspace of crc32c_dev_[copy_]batch_async serves one launch
+ * at a time: a launch on another stream than the previous one waits for it
+ * (use the _ws_ forms with one workspace per stream for concurrency).
  */
 #ifndef PECH_CRC32C_H
 #define PECH_CRC32C_H
@@ -123,6 +127,20 @@ int crc32c_dev_reserve(unsigned int n);
  *                                b = crc32c(0, B), lb = |B|.               */
 uint32_t crc32c_shift(uint32_t v, uint64_t nbytes);
 uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* Drop-in routing: crc32c() calls of at most `bytes` bytes are computed on
+ * the host CPU, larger ones on the GPU (0 = every non-empty call on the GPU).
+ * Default 4 MiB, or the PECH_CRC32C_CPU_MAX environment variable.  Returns
+ * the previous value. */
+unsigned int crc32c_set_cpu_max(unsigned int bytes);
+
+/* Process-wide counters of the drop-in crc32c(). */
+struct crc32c_stats {
+	uint64_t cpu_calls, cpu_bytes;  /* computed on the host (incl. fallbacks) */
+	uint64_t gpu_calls, gpu_bytes;  /* computed by the gfx950 kernels          */
+	uint64_t gpu_fallbacks;         /* GPU path failed, recomputed on the host */
+};
+int crc32c_get_stats(struct crc32c_stats *st);
 
 /* Eagerly initialise the current device (tables, streams).  Optional. */
 int crc32c_device_init(void);

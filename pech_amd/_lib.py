@@ -23,6 +23,12 @@ class CDesc(ctypes.Structure):
     _fields_ = [("addr", ctypes.c_uint64), ("len", ctypes.c_uint32), ("seed", ctypes.c_uint32)]
 
 
+class CStats(ctypes.Structure):
+    """struct crc32c_stats (include/pech_crc32c.h)."""
+    _fields_ = [("cpu_calls", ctypes.c_uint64), ("cpu_bytes", ctypes.c_uint64), ("gpu_calls", ctypes.c_uint64),
+                ("gpu_bytes", ctypes.c_uint64), ("gpu_fallbacks", ctypes.c_uint64)]
+
+
 # completion callback of include/pech_crc32c_async.h: (arg, crc, err)
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int)
 
@@ -45,6 +51,8 @@ SIGNATURES = {
     "crc32c_shift": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
     "crc32c_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     "crc32c_device_init": (ctypes.c_int, []),
+    "crc32c_set_cpu_max": (ctypes.c_uint, [ctypes.c_uint]),
+    "crc32c_get_stats": (ctypes.c_int, [ctypes.c_void_p]),
     "crc32c_timing": (ctypes.c_int, [ctypes.c_int]),
     "crc32c_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
     "crc32c_timing_samples": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.c_uint]),

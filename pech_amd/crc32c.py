@@ -5,7 +5,9 @@ Same names and argument meaning as the reference's crc32c()
 the result is the raw register after the bytes, no inversion.  Device
 buffers are torch uint8 tensors on a ROCm device (torch is plumbing here:
 device memory and streams); every checksum is computed by the gfx950 kernel
-in libpech_crc32c.so.
+in libpech_crc32c.so, except the drop-in crc32c()'s small calls, which the
+library computes on the host as SURVEY.md §8(a) a7/a8 prescribe (see
+set_cpu_max / stats).
 """
 import ctypes
 
@@ -16,7 +18,7 @@ from ._lib import CDesc, Crc32cError, check, lib
 __all__ = [
     "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
     "dev_batch_ws_async", "dev_copy_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
-    "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc",
+    "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc", "set_cpu_max", "stats",
 ]
 
 F_HOST, F_DEVICE, F_PINNED, F_ALL_DEVICES = 0, 1, 2, 4
@@ -30,6 +32,21 @@ def crc32c(crc, data):
         return crc & 0xFFFFFFFF
     buf = (ctypes.c_char * n).from_buffer_copy(mv) if mv.readonly else (ctypes.c_char * n).from_buffer(mv)
     return lib().crc32c(crc & 0xFFFFFFFF, ctypes.addressof(buf), n)
+
+
+def set_cpu_max(nbytes):
+    """Drop-in routing: crc32c() calls of at most nbytes run on the host CPU
+    (0: every non-empty call on the GPU).  Returns the previous value."""
+    return int(lib().crc32c_set_cpu_max(int(nbytes)))
+
+
+def stats():
+    """The drop-in's process-wide counters (struct crc32c_stats) as a dict."""
+    from ._lib import CStats
+
+    st = CStats()
+    check(lib().crc32c_get_stats(ctypes.byref(st)), "crc32c_get_stats")
+    return {name: int(getattr(st, name)) for name, _ in CStats._fields_}
 
 
 def crc32c_batch(bufs, seeds=None):

@@ -18,4 +18,38 @@ PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, 
 // set the thread's crc32c_last_error() text
 PECH_HIDDEN void pech_internal_set_err(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 
+// crc32c_cpu.c: the host routine of the drop-in (small calls, GPU-failure
+// fallback) and the per-thread library stack every HIP-calling entry point
+// runs on (pech's coroutines have 64 KiB stacks, src/sched.c:16)
+extern "C" {
+PECH_HIDDEN uint32_t pech_cpu_crc32c(uint32_t crc, const void *data, size_t n);
+PECH_HIDDEN uint32_t pech_cpu_crc32c_portable(uint32_t crc, const void *data, size_t n);
+PECH_HIDDEN int pech_cpu_has_sse42(void);
+PECH_HIDDEN void pech_stack_call(void (*fn)(void *), void *arg);
+PECH_HIDDEN int pech_on_lib_stack(void);
+}
+
+// f() on the library stack; returns what f returns
+template <class F> static inline auto on_lib_stack(F &&f) -> decltype(f())
+{
+	using R = decltype(f());
+	struct Box {
+		F *f;
+		R r;
+	} box{&f, R{}};
+	pech_stack_call([](void *p) { Box *b = (Box *)p; b->r = (*b->f)(); }, &box);
+	return box.r;
+}
+
+// Fault injection for the failure-path tests (tests/test_faults.py):
+// pech_fault(site) is true on the countdown-th call at that site after
+// crc32c_test_inject(site, countdown) armed it.
+enum pech_fault_site {
+	PECH_FAULT_DROPIN_GPU = 0, // drop-in crc32c(): its GPU launch fails
+	PECH_FAULT_ASYNC_LAUNCH = 1, // async: a slot's kernel launch fails
+	PECH_FAULT_ASYNC_DMA = 2,    // async: a payload's H2D DMA fails
+	PECH_FAULT_SITES = 3
+};
+PECH_HIDDEN bool pech_fault(int site);
+
 #endif

@@ -2,8 +2,14 @@
 // include/pech_crc32c.h): per-device context, constant tables, launch
 // sequencing, host-memory staging pipeline.
 //
-// The only compute path is the gfx950 kernels in crc32c_kernels.hip; this
-// file moves bytes and descriptors and never checksums data on the CPU.
+// Every batch, device and async entry point computes on the gfx950 kernels
+// (crc32c_kernels.hip) and reports a HIP failure as -EIO; this file moves
+// bytes and descriptors.  The one exception is the drop-in crc32c(): like
+// the reference (include/crc32c.h:88-96) it cannot fail, so calls up to
+// crc32c_set_cpu_max() bytes (the messenger's headers, front sections and
+// <=4 KiB pieces) run on the host routine of
+// crc32c_cpu.c, and a failed GPU call is recomputed there (counted in
+// crc32c_get_stats(), reported once on stderr).
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -13,10 +19,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
 #include "../../include/pech_crc32c.h"
+#include "api_internal.h"
 #include "gf2.h"
 #include "layout.h"
 
@@ -88,9 +96,17 @@ struct DevCtx {
 	int dev = -1;
 	int ncu = 0;
 	uint32_t *d_consts = nullptr;
-	// internal workspace for crc32c_dev_batch_async
+	// internal workspace of crc32c_dev_[copy_]batch_async, which run on the
+	// CALLER's streams: the last launch that used it is recorded in ws_ev, and
+	// a launch on another stream waits for it (never two launches at once)
 	void *d_ws = nullptr;
 	size_t ws_bytes = 0;
+	hipEvent_t ws_ev = nullptr;
+	hipStream_t ws_stream = nullptr;
+	bool ws_used = false;
+	// workspace of the synchronous host paths, used on s_comp only
+	void *d_ws_host = nullptr;
+	size_t ws_host_bytes = 0;
 	// synchronous host paths
 	hipStream_t s_comp = nullptr, s_copy[2] = {nullptr, nullptr}; // one copy stream per staging slot
 	uint8_t *h_stage[2] = {nullptr, nullptr};
@@ -160,6 +176,7 @@ static int ctx_get(DevCtx **out)
 			HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
 			HIP_TRY(hipEventCreateWithFlags(&c->ev_done[i], hipEventDisableTiming));
 		}
+		HIP_TRY(hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming));
 		c->dev = dev;
 	}
 	*out = c;
@@ -172,18 +189,51 @@ static size_t ws_bytes_for(unsigned int n)
 	return pech_ws_bytes(n);
 }
 
+// the device-batch workspace (crc32c_dev_[copy_]batch_async): regrown only
+// after the last launch that used it has finished
 static int ws_reserve(DevCtx *c, unsigned int n)
 {
 	const size_t need = ws_bytes_for(n < PECH_MAX_BATCH ? n : PECH_MAX_BATCH);
 	if (need <= c->ws_bytes)
 		return 0;
-	if (c->d_ws)
+	if (c->d_ws) {
+		if (c->ws_used)
+			HIP_TRY(hipEventSynchronize(c->ws_ev));
 		HIP_TRY(hipFree(c->d_ws));
+	}
 	c->d_ws = nullptr;
 	c->ws_bytes = 0;
+	c->ws_used = false;
 	HIP_TRY(hipMalloc(&c->d_ws, need));
 	c->ws_bytes = need;
 	return 0;
+}
+
+// the host paths' workspace, used on s_comp only
+static int ws_host_reserve(DevCtx *c, unsigned int n)
+{
+	const size_t need = ws_bytes_for(n < PECH_MAX_BATCH ? n : PECH_MAX_BATCH);
+	if (need <= c->ws_host_bytes)
+		return 0;
+	if (c->d_ws_host) {
+		HIP_TRY(hipStreamSynchronize(c->s_comp));
+		HIP_TRY(hipFree(c->d_ws_host));
+	}
+	c->d_ws_host = nullptr;
+	c->ws_host_bytes = 0;
+	HIP_TRY(hipMalloc(&c->d_ws_host, need));
+	c->ws_host_bytes = need;
+	return 0;
+}
+
+static bool capturing(hipStream_t s)
+{
+	hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+	if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	return st != hipStreamCaptureStatusNone;
 }
 
 // d_dsts != NULL: fused CRC + copy (d_dsts[i] receives descriptor i's bytes)
@@ -223,9 +273,31 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 	return 0;
 }
 
+// A device batch on the internal workspace, on the caller's stream: ordered
+// after the previous user of the workspace when that was another stream
+// (two streams must never share it concurrently).  Inside a graph
+// capture the caller orders the replays (no event edges into the graph).
+static int launch_internal_ws(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n,
+			      hipStream_t stream, const uint64_t *d_dsts)
+{
+	int rc = ws_reserve(c, n);
+	if (rc)
+		return rc;
+	const bool cap = capturing(stream);
+	if (!cap && c->ws_used && c->ws_stream != stream)
+		HIP_TRY(hipStreamWaitEvent(stream, c->ws_ev, 0));
+	if ((rc = launch_batch(c, d_descs, d_out, n, c->d_ws, c->ws_bytes, stream, d_dsts)))
+		return rc;
+	if (!cap) {
+		HIP_TRY(hipEventRecord(c->ws_ev, stream));
+		c->ws_stream = stream;
+		c->ws_used = true;
+	}
+	return 0;
+}
+
 // ---------------------------------------------------------------------------
 // internal entry points for crc32c_async.cpp (hidden: not part of the C-ABI)
-#include "api_internal.h"
 
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
 				     size_t ws_bytes, hipStream_t stream)
@@ -345,10 +417,10 @@ static int enqueue_host_slot(DevCtx *c, int s, const void *const *bufs, const un
 			       c->s_copy[s]));
 	HIP_TRY(hipEventRecord(c->ev_copied[s], c->s_copy[s]));
 	HIP_TRY(hipStreamWaitEvent(c->s_comp, c->ev_copied[s], 0));
-	int rc = ws_reserve(c, m);
+	int rc = ws_host_reserve(c, m);
 	if (rc)
 		return rc;
-	rc = launch_batch(c, c->d_desc[s], c->d_out[s], m, c->d_ws, c->ws_bytes, c->s_comp);
+	rc = launch_batch(c, c->d_desc[s], c->d_out[s], m, c->d_ws_host, c->ws_host_bytes, c->s_comp);
 	if (rc)
 		return rc;
 	HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
@@ -453,7 +525,7 @@ static int multi_device_pinned(const void *const *bufs, const unsigned int *lens
 			break;
 		if ((rc = stage_reserve(sh[k].c, sh[k].c->stage_bytes ? sh[k].c->stage_bytes : STAGE_BYTES, STAGE_DESCS)))
 			break;
-		if ((rc = ws_reserve(sh[k].c, STAGE_DESCS))) // before any launch: never regrown under one
+		if ((rc = ws_host_reserve(sh[k].c, STAGE_DESCS))) // before any launch: never regrown under one
 			break;
 		for (unsigned int i = cut[k]; i < cut[k + 1]; ++i) {
 			void *dp = nullptr;
@@ -491,7 +563,7 @@ static int multi_device_pinned(const void *const *bufs, const unsigned int *lens
 				break;
 			}
 			// two shards on one device share its stream (ordered), so one workspace serves both
-			if ((rc = launch_batch(c, c->d_desc[s], c->d_out[s], S.m, c->d_ws, c->ws_bytes, c->s_comp)))
+			if ((rc = launch_batch(c, c->d_desc[s], c->d_out[s], S.m, c->d_ws_host, c->ws_host_bytes, c->s_comp)))
 				break;
 			if (hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t)S.m * 4u, hipMemcpyDeviceToHost, c->s_comp) !=
 			    hipSuccess) {
@@ -588,14 +660,97 @@ static int device_batch_sync(DevCtx *c, const void *const *bufs, const unsigned 
 		}
 		HIP_TRY(hipMemcpyAsync(c->d_desc[0], c->h_desc[0], (size_t)m * sizeof(pech_desc), hipMemcpyHostToDevice,
 				       c->s_comp));
-		if ((rc = ws_reserve(c, m)))
+		if ((rc = ws_host_reserve(c, m)))
 			return rc;
-		if ((rc = launch_batch(c, c->d_desc[0], c->d_out[0], m, c->d_ws, c->ws_bytes, c->s_comp)))
+		if ((rc = launch_batch(c, c->d_desc[0], c->d_out[0], m, c->d_ws_host, c->ws_host_bytes, c->s_comp)))
 			return rc;
 		HIP_TRY(hipMemcpyAsync(c->h_out[0], c->d_out[0], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
 		HIP_TRY(hipStreamSynchronize(c->s_comp));
 		memcpy(out + i0, c->h_out[0], (size_t)m * 4u);
 	}
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// drop-in routing, statistics, fault injection
+
+// calls of at most this many bytes run on the host routine; PECH_CRC32C_CPU_MAX
+// overrides the default, crc32c_set_cpu_max() changes it at run time
+static const unsigned int CPU_MAX_DEFAULT = PECH_DROPIN_CPU_MAX_DEFAULT;
+static std::atomic<unsigned int> g_cpu_max{CPU_MAX_DEFAULT};
+static std::once_flag g_cpu_max_env;
+
+static std::atomic<uint64_t> g_st_cpu_calls{0}, g_st_cpu_bytes{0}, g_st_gpu_calls{0}, g_st_gpu_bytes{0},
+	g_st_fallbacks{0};
+static std::atomic<int> g_fault[PECH_FAULT_SITES];
+
+PECH_HIDDEN bool pech_fault(int site)
+{
+	if (site < 0 || site >= PECH_FAULT_SITES)
+		return false;
+	int v = g_fault[site].load(std::memory_order_relaxed);
+	while (v > 0) {
+		if (g_fault[site].compare_exchange_weak(v, v - 1))
+			return v == 1;
+	}
+	return false;
+}
+
+static unsigned int cpu_max()
+{
+	std::call_once(g_cpu_max_env, [] {
+		if (const char *e = getenv("PECH_CRC32C_CPU_MAX")) {
+			char *end = nullptr;
+			const unsigned long long v = strtoull(e, &end, 0);
+			if (end != e)
+				g_cpu_max.store(v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (unsigned int)v);
+		}
+	});
+	return g_cpu_max.load(std::memory_order_relaxed);
+}
+
+// the GPU leg of the drop-in (runs on the library stack)
+static int dropin_gpu(uint32_t crc, const void *data, unsigned int length, uint32_t *out)
+{
+	std::lock_guard<std::mutex> lk(g_mu);
+	DevCtx *c = nullptr;
+	int rc = ctx_get(&c);
+	if (!rc)
+		rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
+	if (rc)
+		return rc;
+	if (pech_fault(PECH_FAULT_DROPIN_GPU)) {
+		set_err("crc32c(): injected GPU failure (test)");
+		return -EIO;
+	}
+	if (length > PECH_SMALL_MAX) {
+		const void *b = data;
+		const uint32_t s = crc;
+		return host_batch(c, &b, &length, &s, out, 1, CRC32C_F_HOST);
+	}
+	// one launch: bytes into pinned staging, read there in place.  The
+	// kernel writes the result, then this call's ticket, to pinned memory;
+	// polling the ticket saves the stream synchronisation (~3 us).  After
+	// ~20 ms of polling the stream is synchronised instead, which also
+	// reports errors.
+	memcpy(c->h_stage[0], data, length);
+	const uint32_t ticket = ++c->small_ticket ? c->small_ticket : ++c->small_ticket;
+	volatile uint32_t *res = (volatile uint32_t *)c->h_small;
+	if (pech_launch_small(c->small_src, length, crc, c->d_consts, c->small_out, ticket, c->s_comp) != hipSuccess) {
+		set_err("small-buffer launch: %s", hipGetErrorString(hipGetLastError()));
+		return -EIO;
+	}
+	for (uint32_t spin = 0; res[1] != ticket && spin < (1u << 22); ++spin)
+		__builtin_ia32_pause();
+	if (res[1] != ticket && hipStreamSynchronize(c->s_comp) != hipSuccess) {
+		set_err("small-buffer kernel: %s", hipGetErrorString(hipGetLastError()));
+		return -EIO;
+	}
+	if (res[1] != ticket) {
+		set_err("small-buffer kernel finished without its result");
+		return -EIO;
+	}
+	*out = res[0];
 	return 0;
 }
 
@@ -607,53 +762,44 @@ uint32_t crc32c(uint32_t crc, const void *data, unsigned int length)
 {
 	if (length == 0)
 		return crc; // include/crc32c.h:92: the loop body never runs
+	if (length <= cpu_max()) {
+		g_st_cpu_calls.fetch_add(1, std::memory_order_relaxed);
+		g_st_cpu_bytes.fetch_add(length, std::memory_order_relaxed);
+		return pech_cpu_crc32c(crc, data, length);
+	}
 	uint32_t out = 0;
-	int rc;
-	{
-		std::lock_guard<std::mutex> lk(g_mu);
-		DevCtx *c = nullptr;
-		rc = ctx_get(&c);
-		if (!rc)
-			rc = stage_reserve(c, STAGE_BYTES, STAGE_DESCS);
-		if (!rc) {
-			if (length <= PECH_SMALL_MAX) {
-				// one launch: bytes into pinned staging, read there in place
-				// The kernel writes the result, then this call's ticket, to
-				// pinned memory; polling the ticket saves the stream
-				// synchronisation (~3 us).  After ~20 ms of polling the
-				// stream is synchronised instead, which also reports errors.
-				memcpy(c->h_stage[0], data, length);
-				const uint32_t ticket = ++c->small_ticket ? c->small_ticket : ++c->small_ticket;
-				volatile uint32_t *res = (volatile uint32_t *)c->h_small;
-				if (pech_launch_small(c->small_src, length, crc, c->d_consts, c->small_out, ticket, c->s_comp) !=
-				    hipSuccess) {
-					set_err("small-buffer launch: %s", hipGetErrorString(hipGetLastError()));
-					rc = -EIO;
-				} else {
-					for (uint32_t spin = 0; res[1] != ticket && spin < (1u << 22); ++spin)
-						__builtin_ia32_pause();
-					if (res[1] != ticket && hipStreamSynchronize(c->s_comp) != hipSuccess) {
-						set_err("small-buffer kernel: %s", hipGetErrorString(hipGetLastError()));
-						rc = -EIO;
-					} else if (res[1] != ticket) {
-						set_err("small-buffer kernel finished without its result");
-						rc = -EIO;
-					} else {
-						out = res[0];
-					}
-				}
-			} else {
-				const void *b = data;
-				const uint32_t s = crc;
-				rc = host_batch(c, &b, &length, &s, &out, 1, CRC32C_F_HOST);
-			}
-		}
+	const int rc = on_lib_stack([&] { return dropin_gpu(crc, data, length, &out); });
+	if (rc == 0) {
+		g_st_gpu_calls.fetch_add(1, std::memory_order_relaxed);
+		g_st_gpu_bytes.fetch_add(length, std::memory_order_relaxed);
+		return out;
 	}
-	if (rc) {
-		fprintf(stderr, "pech_crc32c: crc32c() failed (%d): %s\n", rc, g_err);
-		abort();
+	// total, like the reference: recompute on the host, report once
+	if (g_st_fallbacks.fetch_add(1, std::memory_order_relaxed) == 0)
+		fprintf(stderr, "pech_crc32c: crc32c() GPU path failed (%d: %s); computing on the CPU\n", rc, g_err);
+	g_st_cpu_calls.fetch_add(1, std::memory_order_relaxed);
+	g_st_cpu_bytes.fetch_add(length, std::memory_order_relaxed);
+	return pech_cpu_crc32c(crc, data, length);
+}
+
+unsigned int crc32c_set_cpu_max(unsigned int bytes)
+{
+	(void)cpu_max(); // the environment is read first, so this call wins
+	return g_cpu_max.exchange(bytes);
+}
+
+int crc32c_get_stats(struct crc32c_stats *st)
+{
+	if (!st) {
+		set_err("crc32c_get_stats: null output");
+		return -EINVAL;
 	}
-	return out;
+	st->cpu_calls = g_st_cpu_calls.load();
+	st->cpu_bytes = g_st_cpu_bytes.load();
+	st->gpu_calls = g_st_gpu_calls.load();
+	st->gpu_bytes = g_st_gpu_bytes.load();
+	st->gpu_fallbacks = g_st_fallbacks.load();
+	return 0;
 }
 
 int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds, uint32_t *out,
@@ -667,16 +813,18 @@ int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32
 		set_err("crc32c_batch: invalid arguments");
 		return -EINVAL;
 	}
-	std::lock_guard<std::mutex> lk(g_mu);
-	if (flags & CRC32C_F_ALL_DEVICES)
-		return multi_device_pinned(bufs, lens, seeds, out, n);
-	DevCtx *c = nullptr;
-	int rc = ctx_get(&c);
-	if (rc)
-		return rc;
-	if (flags & CRC32C_F_DEVICE)
-		return device_batch_sync(c, bufs, lens, seeds, out, n);
-	return host_batch(c, bufs, lens, seeds, out, n, flags);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		if (flags & CRC32C_F_ALL_DEVICES)
+			return multi_device_pinned(bufs, lens, seeds, out, n);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		if (flags & CRC32C_F_DEVICE)
+			return device_batch_sync(c, bufs, lens, seeds, out, n);
+		return host_batch(c, bufs, lens, seeds, out, n, flags);
+	});
 }
 
 size_t crc32c_dev_workspace_bytes(unsigned int n)
@@ -693,22 +841,26 @@ int crc32c_dev_batch_ws_async(const struct crc32c_desc *d_descs, uint32_t *d_out
 		set_err("crc32c_dev_batch_ws_async: invalid arguments");
 		return -EINVAL;
 	}
-	std::lock_guard<std::mutex> lk(g_mu);
-	DevCtx *c = nullptr;
-	int rc = ctx_get(&c);
-	if (rc)
-		return rc;
-	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, d_ws, ws_bytes, (hipStream_t)stream);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		return launch_batch(c, (const pech_desc *)d_descs, d_out, n, d_ws, ws_bytes, (hipStream_t)stream);
+	});
 }
 
 int crc32c_dev_reserve(unsigned int n)
 {
-	std::lock_guard<std::mutex> lk(g_mu);
-	DevCtx *c = nullptr;
-	int rc = ctx_get(&c);
-	if (rc)
-		return rc;
-	return ws_reserve(c, n);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		return ws_reserve(c, n);
+	});
 }
 
 int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n, void *stream)
@@ -719,14 +871,14 @@ int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, u
 		set_err("crc32c_dev_batch_async: invalid arguments");
 		return -EINVAL;
 	}
-	std::lock_guard<std::mutex> lk(g_mu);
-	DevCtx *c = nullptr;
-	int rc = ctx_get(&c);
-	if (rc)
-		return rc;
-	if ((rc = ws_reserve(c, n)))
-		return rc;
-	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, c->d_ws, c->ws_bytes, (hipStream_t)stream);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		return launch_internal_ws(c, (const pech_desc *)d_descs, d_out, n, (hipStream_t)stream, nullptr);
+	});
 }
 
 int crc32c_dev_copy_batch_ws_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
@@ -738,12 +890,15 @@ int crc32c_dev_copy_batch_ws_async(const struct crc32c_desc *d_descs, const uint
 		set_err("crc32c_dev_copy_batch_ws_async: invalid arguments");
 		return -EINVAL;
 	}
-	std::lock_guard<std::mutex> lk(g_mu);
-	DevCtx *c = nullptr;
-	int rc = ctx_get(&c);
-	if (rc)
-		return rc;
-	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, d_ws, ws_bytes, (hipStream_t)stream, d_dsts);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		return launch_batch(c, (const pech_desc *)d_descs, d_out, n, d_ws, ws_bytes, (hipStream_t)stream,
+				    d_dsts);
+	});
 }
 
 int crc32c_dev_copy_batch_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
@@ -755,14 +910,14 @@ int crc32c_dev_copy_batch_async(const struct crc32c_desc *d_descs, const uint64_
 		set_err("crc32c_dev_copy_batch_async: invalid arguments");
 		return -EINVAL;
 	}
-	std::lock_guard<std::mutex> lk(g_mu);
-	DevCtx *c = nullptr;
-	int rc = ctx_get(&c);
-	if (rc)
-		return rc;
-	if ((rc = ws_reserve(c, n)))
-		return rc;
-	return launch_batch(c, (const pech_desc *)d_descs, d_out, n, c->d_ws, c->ws_bytes, (hipStream_t)stream, d_dsts);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		return launch_internal_ws(c, (const pech_desc *)d_descs, d_out, n, (hipStream_t)stream, d_dsts);
+	});
 }
 
 uint32_t crc32c_shift(uint32_t v, uint64_t nbytes)
@@ -787,9 +942,11 @@ uint32_t crc32c_concat(uint32_t seed, const uint32_t *crcs, const uint64_t *lens
 
 int crc32c_device_init(void)
 {
-	std::lock_guard<std::mutex> lk(g_mu);
-	DevCtx *c = nullptr;
-	return ctx_get(&c);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		return ctx_get(&c);
+	});
 }
 
 int crc32c_timing(int enable)
@@ -801,28 +958,30 @@ int crc32c_timing(int enable)
 
 int crc32c_timing_read(double *kernel_ms, uint64_t *launches)
 {
-	std::lock_guard<std::mutex> lk(g_mu);
-	double ms = 0;
-	uint64_t cnt = 0;
-	g_samples.clear();
-	for (int d = 0; d < 64; ++d) {
-		DevCtx *c = &g_ctx[d];
-		for (auto &tl : c->pending) {
-			HIP_TRY(hipEventSynchronize(tl.b));
-			float t = 0;
-			HIP_TRY(hipEventElapsedTime(&t, tl.a, tl.b));
-			ms += t;
-			++cnt;
-			g_samples.push_back(t);
-			c->free_events.push_back(tl);
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		double ms = 0;
+		uint64_t cnt = 0;
+		g_samples.clear();
+		for (int d = 0; d < 64; ++d) {
+			DevCtx *c = &g_ctx[d];
+			for (auto &tl : c->pending) {
+				HIP_TRY(hipEventSynchronize(tl.b));
+				float t = 0;
+				HIP_TRY(hipEventElapsedTime(&t, tl.a, tl.b));
+				ms += t;
+				++cnt;
+				g_samples.push_back(t);
+				c->free_events.push_back(tl);
+			}
+			c->pending.clear();
 		}
-		c->pending.clear();
-	}
-	if (kernel_ms)
-		*kernel_ms = ms;
-	if (launches)
-		*launches = cnt;
-	return 0;
+		if (kernel_ms)
+			*kernel_ms = ms;
+		if (launches)
+			*launches = cnt;
+		return 0;
+	});
 }
 
 int crc32c_timing_samples(float *ms, unsigned int max)
@@ -846,6 +1005,35 @@ const char *crc32c_last_error(void)
 const char *crc32c_version(void)
 {
 	return pech_kernel_tag();
+}
+
+// ---- test hooks (tests/test_cpu_path.py, tests/test_faults.py); not in
+// include/: they exercise paths a healthy GPU never takes
+// arm fault `site` (enum pech_fault_site) to fire on its countdown-th use
+int crc32c_test_inject(int site, int countdown)
+{
+	if (site < 0 || site >= PECH_FAULT_SITES)
+		return -EINVAL;
+	g_fault[site].store(countdown);
+	return 0;
+}
+
+// the host routine itself: variant 0 = the one crc32c() uses (SSE4.2 when
+// the CPU has it), 1 = portable slice-by-8
+uint32_t crc32c_test_cpu(uint32_t crc, const void *data, size_t n, int variant)
+{
+	return variant ? pech_cpu_crc32c_portable(crc, data, n) : pech_cpu_crc32c(crc, data, n);
+}
+
+int crc32c_test_cpu_has_sse42(void)
+{
+	return pech_cpu_has_sse42();
+}
+
+// 1 if fn runs on the library stack when called through it (stack switch check)
+int crc32c_test_stack_switch(void)
+{
+	return on_lib_stack([] { return pech_on_lib_stack(); });
 }
 
 } // extern "C"

@@ -20,6 +20,13 @@
 //              in submission order on the caller's thread.
 // No byte is checksummed on the CPU: pieces and combine are GF(2) algebra
 // on kernel results (gf2.h).
+// Every HIP call runs on the library stack (on_lib_stack, crc32c_cpu.c);
+// callbacks run on the caller's own stack, outside the device guard, so a
+// callback may switch coroutines or submit again.
+// Failures: a failed H2D, launch or batch fails every payload with a piece
+// in that slot (callback err = -EIO), makes the context's error sticky and
+// bumps the eventfd so the loop collects them.  A submission that returns
+// an error never gets a callback.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -81,7 +88,7 @@ std::map<uintptr_t, PageAlloc>::iterator find_live(const void *p, size_t len)
 
 } // namespace
 
-extern "C" void *crc32c_pages_alloc(unsigned int order)
+static void *pages_alloc(unsigned int order)
 {
 	if (order > 31u - CRC32C_PAGE_SHIFT) {
 		pech_internal_set_err("crc32c_pages_alloc: order %u too large", order);
@@ -104,10 +111,18 @@ extern "C" void *crc32c_pages_alloc(unsigned int order)
 	return p;
 }
 
-extern "C" void crc32c_pages_free(void *pages, unsigned int order)
+extern "C" void *crc32c_pages_alloc(unsigned int order)
 {
-	if (!pages)
-		return;
+	void *p = nullptr;
+	on_lib_stack([&] {
+		p = pages_alloc(order);
+		return 0;
+	});
+	return p;
+}
+
+static void pages_free(void *pages, unsigned int order)
+{
 	std::lock_guard<std::mutex> lk(g_pages_mu);
 	auto it = g_pages.find((uintptr_t)pages);
 	if (it == g_pages.end() || !it->second.live || it->second.bytes != ((size_t)CRC32C_PAGE_SIZE << order)) {
@@ -124,6 +139,16 @@ extern "C" void crc32c_pages_free(void *pages, unsigned int order)
 	(void)hipHostFree(pages);
 }
 
+extern "C" void crc32c_pages_free(void *pages, unsigned int order)
+{
+	if (!pages)
+		return;
+	on_lib_stack([&] {
+		pages_free(pages, order);
+		return 0;
+	});
+}
+
 extern "C" int crc32c_pages_is_pinned(const void *p, size_t len)
 {
 	std::lock_guard<std::mutex> lk(g_pages_mu);
@@ -132,14 +157,17 @@ extern "C" int crc32c_pages_is_pinned(const void *p, size_t len)
 
 extern "C" void crc32c_pages_trim(void)
 {
-	std::lock_guard<std::mutex> lk(g_pages_mu);
-	for (auto &fl : g_free) {
-		for (void *p : fl) {
-			g_pages.erase((uintptr_t)p);
-			(void)hipHostFree(p);
+	on_lib_stack([] {
+		std::lock_guard<std::mutex> lk(g_pages_mu);
+		for (auto &fl : g_free) {
+			for (void *p : fl) {
+				g_pages.erase((uintptr_t)p);
+				(void)hipHostFree(p);
+			}
+			fl.clear();
 		}
-		fl.clear();
-	}
+		return 0;
+	});
 }
 
 // device address of pinned host bytes p (inside a live allocation), or 0
@@ -208,6 +236,7 @@ struct Item {
 	uint32_t total;     // pieces placed (valid once `placed`)
 	bool placed;        // every piece has been given a descriptor
 	int err;
+	bool cancelled;     // its submit returned an error: no callback
 };
 
 } // namespace
@@ -316,7 +345,12 @@ static int reap(crc32c_async *a, bool wait_oldest)
 				// the host function runs on the runtime's thread: a moment
 			}
 		} else if (!s->finished.load(std::memory_order_acquire)) {
-			return 0;
+			// a failed stream never runs its host function: ask the stream
+			q = hipStreamQuery(s->stream);
+			if (q == hipSuccess || q == hipErrorNotReady) {
+				(void)hipGetLastError();
+				return 0;
+			}
 		}
 		int err = 0;
 		if (q != hipSuccess) {
@@ -359,6 +393,22 @@ static int get_slot(crc32c_async *a, Slot **out)
 	return get_slot(a, out);
 }
 
+// The slot being filled cannot be launched: its payloads fail (err), the
+// context's error becomes sticky, and the eventfd wakes the loop so that
+// crc32c_async_complete() delivers them.
+static int fail_cur_slot(crc32c_async *a, int err)
+{
+	if (Slot *s = a->cur) {
+		harvest(a, s, err);
+		a->cur = nullptr;
+	}
+	a->err = err;
+	const uint64_t one = 1;
+	ssize_t r = write(a->efd, &one, sizeof(one));
+	(void)r;
+	return err;
+}
+
 static int launch_slot(crc32c_async *a)
 {
 	Slot *s = a->cur;
@@ -368,26 +418,30 @@ static int launch_slot(crc32c_async *a)
 	for (auto &r : s->packed)
 		TRY_HIP(hipMemcpyAsync(s->d_stage + r.first, s->h_stage + r.first, r.second - r.first,
 				       hipMemcpyHostToDevice, s->stream),
-			-EIO);
+			fail_cur_slot(a, -EIO));
 	const pech_desc *descs = s->desc_view;
 	if (!descs) {
 		TRY_HIP(hipMemcpyAsync(s->d_desc, s->h_desc, m * sizeof(pech_desc), hipMemcpyHostToDevice, s->stream),
-			-EIO);
+			fail_cur_slot(a, -EIO));
 		descs = s->d_desc;
 	}
 	s->finished.store(0, std::memory_order_relaxed);
+	if (pech_fault(PECH_FAULT_ASYNC_LAUNCH)) {
+		pech_internal_set_err("crc32c_async: injected launch failure (test)");
+		return fail_cur_slot(a, -EIO);
+	}
 	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream);
 	if (rc)
-		return rc;
-	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), -EIO);
-	TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), -EIO);
+		return fail_cur_slot(a, rc);
+	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), fail_cur_slot(a, -EIO));
+	TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_cur_slot(a, -EIO));
 	s->inflight = true;
 	a->inflight.push_back(s);
 	a->cur = nullptr;
 	return 0;
 }
 
-extern "C" struct crc32c_async *crc32c_async_create(unsigned int flags)
+static struct crc32c_async *async_create(unsigned int flags)
 {
 	if (flags & ~CRC32C_ASYNC_ZEROCOPY) {
 		pech_internal_set_err("crc32c_async_create: unknown flags %#x", flags);
@@ -412,30 +466,43 @@ extern "C" struct crc32c_async *crc32c_async_create(unsigned int flags)
 	return a;
 }
 
+extern "C" struct crc32c_async *crc32c_async_create(unsigned int flags)
+{
+	struct crc32c_async *a = nullptr;
+	on_lib_stack([&] {
+		a = async_create(flags);
+		return 0;
+	});
+	return a;
+}
+
 extern "C" int crc32c_async_fd(const struct crc32c_async *a)
 {
 	return a ? a->efd : -EINVAL;
 }
 
-extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsigned int len, uint32_t seed,
-				   crc32c_done_fn done, void *arg)
+static int async_submit(struct crc32c_async *a, const void *buf, unsigned int len, uint32_t seed,
+			crc32c_done_fn done, void *arg)
 {
-	if (!a || !done || (len && !buf)) {
-		pech_internal_set_err("crc32c_async_submit: invalid arguments");
-		return -EINVAL;
-	}
-	if (a->err)
-		return a->err;
 	DeviceGuard dg(a->dev);
 	if (!dg.ok) {
 		pech_internal_set_err("crc32c_async_submit: cannot select device %d", a->dev);
 		return -ENODEV;
 	}
 	const uint64_t id = a->base + a->items.size();
-	a->items.push_back(Item{done, arg, seed, 0u, 0u, false, 0});
+	a->items.push_back(Item{done, arg, seed, 0u, 0u, false, 0, false});
 	const uint8_t *p = (const uint8_t *)buf;
 	size_t left = len;
 	uint32_t placed = 0;
+	// A failure part-way: the pieces already placed complete (with an error
+	// if their slot failed) and the item is retired without a callback.
+	auto fail = [&](int rc) {
+		Item &it = a->items[id - a->base];
+		it.placed = true;
+		it.total = placed;
+		it.cancelled = true;
+		return rc;
+	};
 	// one registry lookup: pinned pages are read in place (zero-copy, below
 	// kZeroCopyMax) or DMA'd
 	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
@@ -445,10 +512,10 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 		Slot *s = nullptr;
 		int rc = get_slot(a, &s);
 		if (rc)
-			return rc;
+			return fail(rc);
 		if (s->pieces.size() == kSlotDescs || (!zc && left && s->used >= kSlotBytes)) {
 			if ((rc = launch_slot(a)))
-				return rc;
+				return fail(rc);
 			continue;
 		}
 		pech_desc &d = s->h_desc[s->pieces.size()];
@@ -460,8 +527,15 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 			piece = left < kSlotBytes - s->used ? left : kSlotBytes - s->used;
 			d.addr = (uint64_t)(uintptr_t)(s->d_stage + s->used);
 			if (piece && dma) {
-				TRY_HIP(hipMemcpyAsync(s->d_stage + s->used, p, piece, hipMemcpyHostToDevice, s->stream),
-					-EIO);
+				hipError_t e = pech_fault(PECH_FAULT_ASYNC_DMA)
+						       ? hipErrorInvalidValue
+						       : hipMemcpyAsync(s->d_stage + s->used, p, piece,
+									hipMemcpyHostToDevice, s->stream);
+				if (e != hipSuccess) {
+					pech_internal_set_err("crc32c_async_submit: payload DMA failed: %s",
+							      hipGetErrorString(e));
+					return fail(fail_cur_slot(a, -EIO));
+				}
 			} else if (piece) {
 				memcpy(s->h_stage + s->used, p, piece);
 				if (!s->packed.empty() && s->packed.back().second == s->used)
@@ -483,8 +557,20 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 	it.total = placed;
 	Slot *s = a->cur;
 	if (s && (s->pieces.size() == kSlotDescs || s->used >= kSlotBytes))
-		return launch_slot(a);
+		return launch_slot(a); // a failure here fails this payload through its callback
 	return 0;
+}
+
+extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsigned int len, uint32_t seed,
+				   crc32c_done_fn done, void *arg)
+{
+	if (!a || !done || (len && !buf)) {
+		pech_internal_set_err("crc32c_async_submit: invalid arguments");
+		return -EINVAL;
+	}
+	if (a->err)
+		return a->err;
+	return on_lib_stack([&] { return async_submit(a, buf, len, seed, done, arg); });
 }
 
 extern "C" int crc32c_async_flush(struct crc32c_async *a)
@@ -493,11 +579,14 @@ extern "C" int crc32c_async_flush(struct crc32c_async *a)
 		return -EINVAL;
 	if (a->err)
 		return a->err;
-	DeviceGuard dg(a->dev);
-	return launch_slot(a);
+	return on_lib_stack([&] {
+		DeviceGuard dg(a->dev);
+		return launch_slot(a);
+	});
 }
 
-// items are finished when every placed piece has been harvested
+// items are finished when every placed piece has been harvested; runs on
+// the caller's stack and device
 static int run_callbacks(crc32c_async *a)
 {
 	int ran = 0;
@@ -508,6 +597,8 @@ static int run_callbacks(crc32c_async *a)
 		const Item done = it;
 		a->items.pop_front();
 		a->base++;
+		if (done.cancelled)
+			continue;
 		done.done(done.arg, done.err ? 0u : done.crc, done.err);
 		++ran;
 	}
@@ -518,12 +609,14 @@ extern "C" int crc32c_async_complete(struct crc32c_async *a)
 {
 	if (!a)
 		return -EINVAL;
-	DeviceGuard dg(a->dev);
-	uint64_t cnt;
-	while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
-	}
-	int rc = reap(a, false);
-	int ran = run_callbacks(a);
+	const int rc = on_lib_stack([&] {
+		DeviceGuard dg(a->dev);
+		uint64_t cnt;
+		while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
+		}
+		return reap(a, false);
+	});
+	const int ran = run_callbacks(a);
 	return rc ? rc : ran;
 }
 
@@ -531,16 +624,21 @@ extern "C" int crc32c_async_drain(struct crc32c_async *a)
 {
 	if (!a)
 		return -EINVAL;
-	DeviceGuard dg(a->dev);
-	int rc = a->err ? a->err : launch_slot(a);
-	while (!a->inflight.empty()) {
-		int r = reap(a, true);
-		if (r && !rc)
-			rc = r;
-	}
-	uint64_t cnt;
-	while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
-	}
+	const int rc = on_lib_stack([&] {
+		DeviceGuard dg(a->dev);
+		int r0 = a->err ? a->err : launch_slot(a);
+		if (a->err && a->cur) // a sticky error: what was never launched fails now
+			fail_cur_slot(a, a->err);
+		while (!a->inflight.empty()) {
+			int r = reap(a, true);
+			if (r && !r0)
+				r0 = r;
+		}
+		uint64_t cnt;
+		while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
+		}
+		return r0;
+	});
 	run_callbacks(a);
 	return rc;
 }
@@ -554,11 +652,14 @@ extern "C" void crc32c_async_destroy(struct crc32c_async *a)
 {
 	if (!a)
 		return;
-	DeviceGuard dg(a->dev >= 0 ? a->dev : 0);
 	if (a->ready)
-		(void)crc32c_async_drain(a);
-	for (Slot *s : a->slots)
-		slot_free(s); // synchronises the slot's stream first
+		(void)crc32c_async_drain(a); // callbacks on the caller's stack
+	on_lib_stack([&] {
+		DeviceGuard dg(a->dev >= 0 ? a->dev : 0);
+		for (Slot *s : a->slots)
+			slot_free(s); // synchronises the slot's stream first
+		return 0;
+	});
 	if (a->efd >= 0)
 		close(a->efd);
 	delete a;

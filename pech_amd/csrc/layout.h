@@ -36,6 +36,7 @@
 #define PECH_LARGE_ROWS 2048u     /* size-class cap for the plan's ordering  */
 #define PECH_SPLIT_ROWS 256u      /* >= this: a buffer is split over 8 groups */
 #define PECH_SMALL_MAX 65536u     /* drop-in crc32c(): one-launch path up to this */
+#define PECH_DROPIN_CPU_MAX_DEFAULT (4u << 20) /* drop-in crc32c(): host routine up to this */
 /* payload of one launch: rows (128 B) are counted in 32 bits, so < 512 GiB */
 #define PECH_LAUNCH_MAX_BYTES (256ull << 30)
 

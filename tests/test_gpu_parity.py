@@ -30,6 +30,20 @@ def P():
     return pech_amd
 
 
+@pytest.fixture
+def gpu_route(P):
+    """Route every non-empty drop-in crc32c() call to the GPU for the test and
+    check afterwards that the kernels computed them (no host fallback)."""
+    prev = P.set_cpu_max(0)
+    before = P.stats()
+    yield
+    P.set_cpu_max(prev)
+    after = P.stats()
+    assert after["gpu_fallbacks"] == before["gpu_fallbacks"], after
+    assert after["gpu_calls"] > before["gpu_calls"], after
+    assert after["cpu_calls"] == before["cpu_calls"], after
+
+
 def dev_crcs(torch, P, dbuf, offs, lens, seeds=None):
     """kernel CRCs of dbuf[off:off+len] (dbuf: device uint8 tensor)."""
     base = dbuf.data_ptr()
@@ -222,7 +236,7 @@ def test_more_than_one_launch_of_buffers(torch_dev, P):
     assert np.array_equal(got, O.crcs(host, offs, lens))
 
 
-def test_dropin_crc32c_host_memory(P):
+def test_dropin_crc32c_host_memory(P, gpu_route):
     rng = np.random.default_rng(8)
     for n in (1, 3, 4, 49, 4096, 100000):
         d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
@@ -231,9 +245,9 @@ def test_dropin_crc32c_host_memory(P):
     assert P.crc32c(0x1234, b"") == 0x1234
 
 
-def test_dropin_small_path_boundaries(P):
-    # crc32c() up to PECH_SMALL_MAX (64 KiB) is one zero-copy launch; above
-    # it the staged batch path.  Sizes around both paths' edges, unaligned
+def test_dropin_small_path_boundaries(P, gpu_route):
+    # On the GPU route, crc32c() up to PECH_SMALL_MAX (64 KiB) is one
+    # zero-copy launch; above it the staged batch path.  Sizes around both paths' edges, unaligned
     # sources, random seeds
     rng = np.random.default_rng(18)
     big = rng.integers(0, 256, (1 << 17) + 64, dtype=np.uint8)
@@ -244,7 +258,7 @@ def test_dropin_small_path_boundaries(P):
             assert P.crc32c(s, d) == O.crc(s, d), (n, off)
 
 
-def test_dropin_crc32c_larger_than_staging(P):
+def test_dropin_crc32c_larger_than_staging(P, gpu_route):
     # > 64 MiB staging slot: chained through the seed inside the library
     d = np.random.default_rng(9).integers(0, 256, (64 << 20) + 4097, dtype=np.uint8)
     assert P.crc32c(0xFFFFFFFF, d) == O.crc(0xFFFFFFFF, d)
@@ -382,3 +396,60 @@ def test_graph_capture_and_replay(torch_dev, P):
     g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), O.crcs(buf.cpu().numpy(), offs, [L] * n))
+
+
+def test_dropin_default_route(P):
+    # default routing: headers / front sections / <=4 KiB pieces (and every
+    # call up to 4 MiB) on the host routine, larger calls on the GPU
+    rng = np.random.default_rng(31)
+    before = P.stats()
+    for n in (49, 4096, 65536, 4 << 20):
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        assert P.crc32c(5, d) == O.crc(5, d)
+    mid = P.stats()
+    assert mid["cpu_calls"] - before["cpu_calls"] == 4 and mid["gpu_calls"] == before["gpu_calls"]
+    d = rng.integers(0, 256, (4 << 20) + 1, dtype=np.uint8)
+    assert P.crc32c(6, d) == O.crc(6, d)
+    after = P.stats()
+    assert after["gpu_calls"] == mid["gpu_calls"] + 1 and after["gpu_fallbacks"] == before["gpu_fallbacks"]
+
+
+def test_dropin_concurrent_with_device_batch(torch_dev, P, gpu_route):
+    # a drop-in / host batch call while a device batch is in
+    # flight on another stream must not share its workspace
+    torch, dev = torch_dev
+    n, L = 4096, 65536
+    buf = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+    offs = np.arange(n) * L
+    descs = P.make_descs([buf.data_ptr() + int(o) for o in offs], [L] * n, device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    host = np.random.default_rng(32).integers(0, 256, 1 << 20, dtype=np.uint8)
+    s = torch.cuda.Stream(dev)
+    want_host = O.crc(3, host)
+    for _ in range(3):
+        P.dev_batch_async(descs, out, stream=s)  # 256 MiB in flight
+        assert P.crc32c(3, host) == want_host    # staged host path meanwhile
+        assert P.crc32c_batch([host.tobytes()], [3]) == [want_host]
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), O.crcs(buf.cpu().numpy(), offs, [L] * n))
+
+
+def test_internal_workspace_two_streams(torch_dev, P):
+    # two device batches on the INTERNAL workspace from two streams: the
+    # second waits for the first instead of overwriting its workspace
+    torch, dev = torch_dev
+    jobs = []
+    for k, (n, L) in enumerate(((2048, 65536), (64, 4 << 20))):
+        buf = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
+        offs = np.arange(n) * L
+        descs = P.make_descs([buf.data_ptr() + int(o) for o in offs], [L] * n, [k] * n, device=dev)
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        jobs.append((buf, offs, L, k, descs, out, torch.cuda.Stream(dev)))
+    torch.cuda.synchronize()
+    for _ in range(4):
+        for buf, offs, L, k, descs, out, st in jobs:
+            P.dev_batch_async(descs, out, stream=st)
+    torch.cuda.synchronize()
+    for buf, offs, L, k, descs, out, st in jobs:
+        want = O.crcs(buf.cpu().numpy(), offs, [L] * len(offs), [k] * len(offs))
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
