@@ -11,7 +11,7 @@ HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h pech_amd/csrc/api_internal.h in
 LIB = pech_amd/libpech_crc32c.so
 OBJ = build/crc32c_kernels.o build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
 
-all: $(LIB) oracle build/msgr_sim build/dropin_kat build/coro_stack
+all: $(LIB) oracle build/msgr_sim build/dropin_kat build/coro_stack build/dropin_bench
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -65,6 +65,12 @@ build/coro_stack: tests/c/coro_stack.c oracle/crc32c_oracle.c include/pech_crc32
 	@mkdir -p build
 	gcc -std=gnu89 -O2 -Wall -Werror -U_FORTIFY_SOURCE -D_FORTIFY_SOURCE=0 -Iinclude tests/c/coro_stack.c oracle/crc32c_oracle.c -Lpech_amd \
 		-lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
+
+# bench tool: drop-in per-call latency, host vs GPU route vs the reference loop
+build/dropin_bench: tools/c/dropin_bench.c oracle/crc32c_oracle.c include/pech_crc32c.h $(LIB)
+	@mkdir -p build
+	gcc -std=gnu89 -O2 -Wall -Werror -fno-strict-aliasing -Iinclude tools/c/dropin_bench.c oracle/crc32c_oracle.c \
+		-Lpech_amd -lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
 
 oracle:
 	$(MAKE) -C oracle all

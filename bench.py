@@ -34,6 +34,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -316,26 +317,20 @@ def host_path(args, buf0, offs, sizes, outs, P):
 
 
 def dropin_latency(P):
-    """Per-call latency of the drop-in crc32c() (pageable host memory, one
-    synchronous call per buffer, as messenger.c calls it per header and per
-    <=4 KiB piece).  Each size's result is checked against crc32c_batch on
-    the same bytes (the staged batch path)."""
-    from pech_amd import _lib
-
-    lib = _lib.lib()
-    res = {}
-    for n in (49, 4096, 65536):
-        buf = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
-        p = buf.ctypes.data
-        if lib.crc32c(0, p, n) != P.crc32c_batch([buf.tobytes()])[0]:
-            raise SystemExit("PARITY FAILURE: drop-in crc32c() differs from crc32c_batch")
-        t = []
-        for _ in range(300):
-            t0 = time.perf_counter()
-            lib.crc32c(0, p, n)
-            t.append(time.perf_counter() - t0)
-        res[str(n)] = round(float(np.median(t)) * 1e6, 2)
-    return {"p50_us_by_bytes": res, "path": "crc32c(0, buf, n) from pageable memory, synchronous"}
+    """Per-call latency of the drop-in crc32c() from C (build/dropin_bench,
+    tools/c/dropin_bench.c): pageable host memory, one synchronous call per
+    buffer as messenger.c calls it per header / section / <=4 KiB piece.
+    Columns: "host" = default routing (host routine up to 4 MiB, GPU above),
+    "gpu" = every call through the gfx950 kernels, "ref" = the reference
+    byte loop.  The tool checks every route against the reference."""
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "dropin_bench")
+    r = subprocess.run([exe, "0.1"], capture_output=True, timeout=300)
+    if r.returncode != 0:
+        raise SystemExit("PARITY FAILURE (drop-in): " + r.stdout.decode() + r.stderr.decode())
+    res = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    res["path"] = ("crc32c(0, buf, n) from pageable memory, synchronous, called from C; host = default "
+                   "routing (<= 4 MiB on the host routine), gpu = crc32c_set_cpu_max(0), ref = reference loop")
+    return res
 
 
 def msgr_path(args, buf0, offs, sizes, outs, P):
