@@ -11,7 +11,7 @@ HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h pech_amd/csrc/api_internal.h in
 LIB = pech_amd/libpech_crc32c.so
 OBJ = build/crc32c_kernels.o build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
 
-all: $(LIB) oracle build/msgr_sim build/dropin_kat build/coro_stack build/dropin_bench
+all: $(LIB) oracle build/msgr_sim build/dropin_kat build/coro_stack build/dropin_bench build/lib_dbg.so
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -44,6 +44,13 @@ variant: build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
 	$(HIPCC) $(HIPFLAGS) $(D) -c pech_amd/csrc/crc32c_kernels.hip -o build/k_$(V).o
 	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o build/crc32c_api.o build/crc32c_async.o \
 		build/crc32c_cpu.o
+
+# bounds-checked kernel build for the GPU test suite (tests/test_gpu_bounds.py):
+# every ring load is checked against its buffer's core; a violation prints
+# "PECH OOB" and is redirected instead of faulting
+build/lib_dbg.so: pech_amd/csrc/crc32c_kernels.hip $(HDR) build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
+	$(HIPCC) $(HIPFLAGS) -DPECH_DEBUG_BOUNDS -c pech_amd/csrc/crc32c_kernels.hip -o build/k_dbg.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/k_dbg.o build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
 
 # test program: pech's receive path on the async layer (gnu89, epoll loop);
 # links the test oracle for the expected footer CRCs -- not product code

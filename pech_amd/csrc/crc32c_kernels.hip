@@ -43,23 +43,11 @@
 #define PECH_MAIN_WAVES 16 // waves per main-kernel workgroup (one workgroup per CU)
 #endif
 #define PECH_MAIN_THREADS (64u * PECH_MAIN_WAVES)
-// Rows of a workgroup's range per wave, by the wave's age rank on its SIMD
-// (wave k of the workgroup runs on SIMD k%4 with rank k/4).  The SIMD issues
-// oldest-first, so with equal shares the youngest waves finish last
-// (measured with -DPECH_STAMPS on C3: ranks 0..3 end at 87/112/140/158 us).
-#ifndef PECH_SLOT_W0
-#define PECH_SLOT_W0 16
+// Diagnostic switches that change results exist only with PECH_DIAG (A/B
+// builds, tools/build_ab.sh): a product build that sees one fails here.
+#if (defined(PECH_AB_NOLDS) || defined(PECH_AB_NOLOAD)) && !defined(PECH_DIAG)
+#error "PECH_AB_NOLDS / PECH_AB_NOLOAD produce wrong CRCs: diagnostic builds must also define PECH_DIAG"
 #endif
-#ifndef PECH_SLOT_W1
-#define PECH_SLOT_W1 16
-#endif
-#ifndef PECH_SLOT_W2
-#define PECH_SLOT_W2 16
-#endif
-#ifndef PECH_SLOT_W3
-#define PECH_SLOT_W3 16
-#endif
-
 
 // Split-step results are XORed into a workgroup table in LDS and reach out[]
 // with one global atomic per (workgroup, buffer), issued by the workgroup's
@@ -440,8 +428,6 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 #define LD_PIECE(S, a, tag) ld_piece((a), (S).blo, (S).bhi, (tag))
 #elif defined(PECH_AB_NOLOAD) // diagnostic build only: no HBM reads (wrong CRCs)
 #define LD_PIECE(S, a, tag) ((u32x4)((uint32_t)(a)))
-#elif defined(PECH_TEMPORAL_LOADS) // A/B: default cache policy
-#define LD_PIECE(S, a, tag) (*(g_u32x4 *)(a))
 #else // payload bytes are read once: nontemporal (measured +8-10 % HBM rate)
 #define LD_PIECE(S, a, tag) (__builtin_nontemporal_load((g_u32x4 *)(a)))
 #endif
@@ -490,30 +476,7 @@ __device__ __forceinline__ void find_start_wave(const uint32_t *__restrict__ lrs
 	lr = uni(rr - lo);
 }
 
-// s_setprio takes an immediate: wave-uniform branch over the 4 levels
-__device__ __forceinline__ void set_prio(uint32_t p)
-{
-	if (p == 0)
-		__builtin_amdgcn_s_setprio(0);
-	else if (p == 1)
-		__builtin_amdgcn_s_setprio(1);
-	else if (p == 2)
-		__builtin_amdgcn_s_setprio(2);
-	else
-		__builtin_amdgcn_s_setprio(3);
-}
-
-// Cumulative share weight of the workgroup's waves 0..k-1 (PECH_SLOT_W*).
 static_assert(PECH_MAIN_WAVES % 4 == 0 && PECH_MAIN_WAVES <= 16, "waves per workgroup: 4, 8, 12 or 16");
-__device__ __forceinline__ uint32_t slot_cw(uint32_t k)
-{
-	const uint32_t w[4] = {PECH_SLOT_W0, PECH_SLOT_W1, PECH_SLOT_W2, PECH_SLOT_W3};
-	uint32_t c = 0;
-#pragma unroll
-	for (uint32_t g = 0; g < 4u; ++g)
-		c += w[g] * min(4u, k > 4u * g ? k - 4u * g : 0u);
-	return c;
-}
 
 // Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
 // the destination offset of each group's buffer (deltas[orig], scalar loads).
@@ -765,13 +728,8 @@ template <bool COPY>
 __device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, bool ok)
 {
 	typedef __attribute__((address_space(1))) u32x4 g_u32x4w;
-#ifdef PECH_TEMPORAL_STORES // A/B: default cache policy for the copy's stores
-	if (COPY && ok)
-		*(g_u32x4w *)(S.dad + (uint64_t)row * PECH_ROW_BYTES) = v;
-#else
-	if (COPY && ok)
+	if (COPY && ok) // nontemporal: the destination is not re-read by this launch
 		__builtin_nontemporal_store(v, (g_u32x4w *)(S.dad + (uint64_t)row * PECH_ROW_BYTES));
-#endif
 }
 
 template <bool COPY, uint32_t U>
@@ -783,9 +741,6 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 {
 	const uint32_t tid = threadIdx.x;
 	STAMP(t_entry);
-#ifdef PECH_PROLOGUE_PRIO // A/B: prologue at raised issue priority, back to 0 for the row loops
-	__builtin_amdgcn_s_setprio(3);
-#endif
 
 	// Table constants first: their loads (L2/MALL) overlap the chunk-count
 	// loads below, and the LDS fill is done before the scan's barriers --
@@ -870,10 +825,11 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t wave = uni(tid >> 6);
 	u32x4 ring[U];
 	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
-	// contiguous pieces weighted by age rank (see PECH_SLOT_W*).
+	// equal contiguous pieces (age-weighted shares measured no better,
+	// profiles/r01/ab_v5.txt).
 	const uint32_t wg_rows = (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
-	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * slot_cw(wave) / slot_cw(PECH_MAIN_WAVES));
-	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * slot_cw(wave + 1u) / slot_cw(PECH_MAIN_WAVES));
+	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
+	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
 	const uint32_t rem_all = r1 - r0;
 	uint32_t p0 = 0, lr0 = 0;
 	if (rem_all)
@@ -890,15 +846,6 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// as soon as its prime is issued (a barrier cost 1-2 us of prologue).
 
 	STAMP(t_start);
-#ifdef PECH_PROLOGUE_PRIO
-	__builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef PECH_PRELOOP_BARRIER // A/B: every wave of the workgroup primed before any streams
-	__syncthreads();
-#endif
-#ifdef PECH_PRIO_YOUNG // diagnostic: younger waves (higher age rank on the SIMD) issue first
-	set_prio(wave >> 2);
-#endif
 #ifdef PECH_STAMPS
 	uint64_t tq[3] = {0, 0, 0};
 	uint32_t nstep = 0;
@@ -916,9 +863,6 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifdef PECH_STAMPS
 			if (nstep == 0 && (blk == nblk / 4u || blk == nblk / 2u || blk == 3u * nblk / 4u))
 				tq[blk == nblk / 4u ? 0 : (blk == nblk / 2u ? 1 : 2)] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef PECH_PRIO_ROTATE // diagnostic: rotate issue priority among the SIMD's waves every block
-			set_prio((blk + (wave >> 2)) & 3u);
 #endif
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {

@@ -25,7 +25,7 @@ def _consts():
     out["PECH_U"] = int(re.search(r"#define PECH_U (\d+)", ksrc).group(1))
     out["PECH_U_COPY"] = int(re.search(r"#define PECH_U_COPY (\d+)", ksrc).group(1))
     out["PECH_MAIN_WAVES"] = int(re.search(r"#define PECH_MAIN_WAVES (\d+)", ksrc).group(1))
-    out["PECH_SLOT_W"] = [int(re.search(r"#define PECH_SLOT_W%d (\d+)" % g, ksrc).group(1)) for g in range(4)]
+    out["PECH_SLOT_W"] = [1, 1, 1, 1]  # the kernel splits a workgroup's rows equally over its waves
     return out
 
 

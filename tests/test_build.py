@@ -129,3 +129,52 @@ def test_loops_with_ring_loads_never_wait_for_zero(device_asm, kernel):
         checked += 1
         assert not [l for l in region if "vmcnt(0)" in l], (kernel, label)
     assert checked >= 1, (kernel, checked)  # the step loop, which holds every row loop
+
+
+def _hipcc():
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    return hipcc
+
+
+@pytest.mark.parametrize("flag", ["-DPECH_AB_NOLDS", "-DPECH_AB_NOLOAD"])
+def test_result_changing_switches_need_pech_diag(flag):
+    # a stray diagnostic -D must not build a library that returns wrong CRCs
+    r = subprocess.run([_hipcc(), "-E", "--offload-arch=gfx950", "--cuda-device-only", flag, SRC, "-o", os.devnull],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "PECH_DIAG" in r.stderr
+    r = subprocess.run([_hipcc(), "-E", "--offload-arch=gfx950", "--cuda-device-only", flag, "-DPECH_DIAG", SRC,
+                        "-o", os.devnull], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_release_library_is_not_a_diagnostic_build():
+    lib = os.path.join(REPO, "pech_amd", "libpech_crc32c.so")
+    if not os.path.exists(lib):
+        pytest.skip("library not built")
+    blob = open(lib, "rb").read()
+    assert b"PECH OOB" not in blob          # not the bounds-checked build
+    assert b"pech_stamps" not in blob       # not the stamps build
+    assert b"pech_read_stamps" not in blob
+
+
+def test_row_addr_launder_survives(device_asm):
+    """row_addr() launders the row-0 address through an empty asm: without it
+    LLVM folded ad + zoff back to ad for virtual leading pieces (a read
+    before the buffer; a GPU fault at allocation starts in r01).  The launder
+    shows as inline-asm markers in the main kernels' ISA, and each one's
+    output feeds a ring load."""
+    asm, _ = device_asm
+    for kernel in ("pech_crc32c_main", "pech_crc32c_main_copy"):
+        body = kernel_body(asm, kernel)
+        n = body.count(";;#ASMSTART")
+        assert n >= 4, (kernel, n)
+        lines = [l.strip() for l in body.split("\n")]
+        fed = 0
+        for i, l in enumerate(lines):
+            if l.startswith(";;#ASMEND"):
+                nxt = lines[i + 1:i + 40]
+                if any(x.startswith("global_load_dwordx4") for x in nxt):
+                    fed += 1
+        assert fed >= 4, (kernel, fed, n)

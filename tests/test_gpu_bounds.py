@@ -1,0 +1,58 @@
+"""The bounds-checked kernel build (build/lib_dbg.so, -DPECH_DEBUG_BOUNDS,
+built by `make`) on C4- and C2-shaped batches with unaligned starts and
+ragged ends: every ring load is checked against its buffer's core on the
+GPU (a violation prints "PECH OOB" and is redirected instead of faulting),
+and every result must still equal the oracle.  Runs in a subprocess so the
+release library stays the one this test process loads."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, "tests")
+import oracle_lib as O
+import pech_amd as P
+assert P._lib.LIB_PATH.endswith("lib_dbg.so"), P._lib.LIB_PATH
+dev = torch.device("cuda:0")
+rng = np.random.default_rng(int(sys.argv[1]))
+shape = sys.argv[2]
+if shape == "c4":
+    lens = np.array([4096] * 2048 + [65536] * 128 + [1 << 20] * 8 + [4 << 20] * 2, dtype=np.int64)
+    lens = lens + rng.integers(-15, 16, lens.size)       # ragged ends
+else:
+    lens = np.array([4096] * 8192, dtype=np.int64) + rng.integers(-33, 34, 8192)
+rng.shuffle(lens)
+offs = np.cumsum(np.concatenate([[7], lens[:-1] + rng.integers(1, 40, lens.size - 1)]))
+host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+seeds = rng.integers(0, 1 << 32, lens.size, dtype=np.uint64)
+buf = torch.from_numpy(host).to(dev)
+descs = P.make_descs(buf.data_ptr() + offs, lens, seeds, device=dev)
+out = torch.zeros(lens.size, dtype=torch.int32, device=dev)
+P.dev_batch_async(descs, out)
+torch.cuda.synchronize()
+got = out.cpu().numpy().view(np.uint32)
+assert np.array_equal(got, O.crcs(host, offs, lens, seeds)), "parity"
+print("ok", lens.size, int(lens.sum()))
+"""
+
+
+@pytest.mark.parametrize("seed,shape", [(1, "c4"), (2, "c2"), (3, "c4")])
+def test_bounds_checked_build(seed, shape):
+    lib = os.path.join(REPO, "build", "lib_dbg.so")
+    assert os.path.exists(lib), "build/lib_dbg.so is built by `make`"
+    env = dict(os.environ, PECH_CRC32C_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", SCRIPT, str(seed), shape], cwd=REPO, env=env, capture_output=True,
+                       timeout=300)
+    out = r.stdout.decode() + r.stderr.decode()
+    assert "PECH OOB" not in out, out[-3000:]
+    assert r.returncode == 0, out[-3000:]
+    assert "ok" in r.stdout.decode()

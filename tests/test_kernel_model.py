@@ -86,6 +86,7 @@ def test_one_buffer_many_waves():
 
 @pytest.mark.parametrize("weights", [[16, 12, 9, 8], [16, 1, 1, 1], [1, 1, 1, 16]])
 def test_weighted_shares(weights):
+    # any contiguous split of a workgroup's rows is valid (the kernel uses equal shares)
     sizes = [4096] * 300 + [300000] * 2 + [100] * 40
     random.Random(5).shuffle(sizes)
     descs, base = [], 1 << 16
