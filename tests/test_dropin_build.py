@@ -86,4 +86,4 @@ def test_pech_osd_links_and_binds_to_library():
         r = subprocess.run([exe], capture_output=True, text=True, timeout=60, env=env)
         lines = [l for l in r.stderr.splitlines() if "`crc32c'" in l]
         assert lines and all("libpech_crc32c.so" in l for l in lines), lines or r.stderr[-2000:]
-        assert "mon_addrs" in r.stderr
+        assert "mon_addrs" in r.stdout + r.stderr
