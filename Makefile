@@ -4,14 +4,16 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
 SRC = pech_amd/csrc/crc32c_kernels.hip pech_amd/csrc/crc32c_api.cpp pech_amd/csrc/crc32c_async.cpp \
-      pech_amd/csrc/crc32c_cpu.c
+      pech_amd/csrc/crc32c_cpu.c pech_amd/csrc/crc32c_msgr.c
 CFLAGS_HOST ?= -O2 -std=gnu11 -fPIC -Wall -Wextra -Werror
 HDR = pech_amd/csrc/gf2.h pech_amd/csrc/layout.h pech_amd/csrc/api_internal.h include/crc32c.h include/pech_crc32c.h \
-      include/pech_crc32c_async.h
+      include/pech_crc32c_async.h include/pech_crc32c_msgr.h
 LIB = pech_amd/libpech_crc32c.so
-OBJ = build/crc32c_kernels.o build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
+HOST_OBJ = build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o build/crc32c_msgr.o
+OBJ = build/crc32c_kernels.o $(HOST_OBJ)
 
-all: $(LIB) oracle build/msgr_sim build/dropin_kat build/coro_stack build/dropin_bench build/lib_dbg.so
+all: $(LIB) oracle build/msgr_sim build/msgr_conn_sim build/dropin_kat build/coro_stack build/dropin_bench \
+     build/lib_dbg.so
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -30,6 +32,10 @@ build/crc32c_cpu.o: pech_amd/csrc/crc32c_cpu.c pech_amd/csrc/gf2.h
 	@mkdir -p build
 	gcc $(CFLAGS_HOST) -c $< -o $@
 
+build/crc32c_msgr.o: pech_amd/csrc/crc32c_msgr.c include/pech_crc32c_msgr.h include/pech_crc32c_async.h
+	@mkdir -p build
+	gcc $(CFLAGS_HOST) -c $< -o $@
+
 $(LIB): $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
 
@@ -40,17 +46,16 @@ asm: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 		../pech_amd/csrc/crc32c_kernels.hip -o crc32c_kernels.s
 
 # A/B diagnostic build: make variant V=name D="-DPECH_U=9" -> build/lib_name.so
-variant: build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
+variant: $(HOST_OBJ)
 	$(HIPCC) $(HIPFLAGS) $(D) -c pech_amd/csrc/crc32c_kernels.hip -o build/k_$(V).o
-	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o build/crc32c_api.o build/crc32c_async.o \
-		build/crc32c_cpu.o
+	$(HIPCC) $(HIPFLAGS) -shared -o build/lib_$(V).so build/k_$(V).o $(HOST_OBJ)
 
 # bounds-checked kernel build for the GPU test suite (tests/test_gpu_bounds.py):
 # every ring load is checked against its buffer's core; a violation prints
 # "PECH OOB" and is redirected instead of faulting
-build/lib_dbg.so: pech_amd/csrc/crc32c_kernels.hip $(HDR) build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
+build/lib_dbg.so: pech_amd/csrc/crc32c_kernels.hip $(HDR) $(HOST_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DPECH_DEBUG_BOUNDS -c pech_amd/csrc/crc32c_kernels.hip -o build/k_dbg.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/k_dbg.o build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/k_dbg.o $(HOST_OBJ)
 
 # test program: pech's receive path on the async layer (gnu89, epoll loop);
 # links the test oracle for the expected footer CRCs -- not product code
@@ -59,6 +64,13 @@ build/msgr_sim: tests/c/msgr_sim.c oracle/crc32c_oracle.c include/pech_crc32c_as
 	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
 		tests/c/msgr_sim.c oracle/crc32c_oracle.c -Lpech_amd -lpech_crc32c -L/opt/rocm/lib -lamdhip64 \
 		-Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
+
+# test program: messenger connection state machine on the adapter (send, receive
+# verify queue, faults and resends, REPOP fan-out, option gates)
+build/msgr_conn_sim: tests/c/msgr_conn_sim.c oracle/crc32c_oracle.c include/pech_crc32c_msgr.h $(LIB)
+	@mkdir -p build
+	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude tests/c/msgr_conn_sim.c oracle/crc32c_oracle.c -Lpech_amd \
+		-lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
 
 # test program: the drop-in crc32c() from C, as messenger.c calls it
 build/dropin_kat: tests/c/dropin_kat.c include/crc32c.h $(LIB)

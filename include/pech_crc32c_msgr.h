@@ -1,0 +1,128 @@
+/*
+ * pech_crc32c_msgr.h -- the messenger-side adapter of libpech_crc32c.so:
+ * GPU data CRCs that keep the messenger's sequencing and ack semantics.
+ *
+ * The async layer (pech_crc32c_async.h) completes payload CRCs later, on the
+ * epoll loop.  The messenger cannot simply "verify in the callback":
+ *  - process_message() consumes con->in_msg and bumps in_seq
+ *    (/root/reference/src/ceph/messenger.c:2858-2869), and
+ *    prepare_read_message() requires in_msg == NULL (:1882), so the next
+ *    message cannot be read while one waits in in_msg;
+ *  - in_seq is what prepare_write_ack() acknowledges (:1444-1454, :3013):
+ *    acking a message whose data CRC has not been checked yet would let the
+ *    peer drop it, and a later mismatch (:2838-2842) would lose it;
+ *  - the footer goes on the wire after the data (:1793-1798), so the send
+ *    side needs the CRC by the time the last data byte is written.
+ * This adapter gives each connection
+ *  RECEIVE: a verify queue.  When a message's footer has been read the
+ *    messenger detaches it from in_msg into the queue (crc32c_msgr_rx_queue:
+ *    the GPU CRC is submitted there), keeps reading, and dispatches from the
+ *    queue head in arrival order (crc32c_msgr_rx_next) -- in_seq, and so the
+ *    ack, advances only for verified messages.  A mismatch at the head is
+ *    reported as -EBADMSG: the connection faults exactly as today, the peer
+ *    resends everything unacked, and crc32c_msgr_conn_reset() drops the
+ *    queue (buffers still being read by the GPU are released when their CRC
+ *    completes, never before).
+ *  SEND: the data CRC is submitted when the message is prepared
+ *    (prepare_write_message, :1345-1439), before its first byte is sent, and
+ *    collected at the footer (crc32c_msgr_tx_footer); if it is not ready the
+ *    connection holds the footer and is kicked when it is.  A CRC known
+ *    without a data pass -- the REPOP fan-out (osd_server.c:1119, :1972)
+ *    forwards the verified request data to every replica -- is registered
+ *    with crc32c_msgr_tx_known(): no GPU work per replica.
+ * The option gates stay in the messenger (CEPH_OPT_NO_DATA_CRC, libceph.h:36):
+ * with data CRCs off it passes check = 0 / never submits, and sets
+ * CEPH_MSG_FOOTER_NOCRC as today.
+ *
+ * Ownership: every message handed to the adapter (rx_queue, tx_submit,
+ * tx_known) comes back exactly once -- from rx_next, from tx_footer (1), or
+ * through release() -- and its data must stay valid and unchanged until then.
+ * GPU failures never reach the messenger: a refused submission or a failed
+ * batch is recomputed on the host from the same bytes.
+ * Threading: as the async layer -- one caller thread; the kick and release
+ * callbacks run inside crc32c_async_complete() on that thread (release also
+ * inside reset / destroy).
+ * Errors: 0 / negative errno (include/err.h style).
+ */
+#ifndef PECH_CRC32C_MSGR_H
+#define PECH_CRC32C_MSGR_H
+
+#include <stdint.h>
+
+#include "pech_crc32c_async.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct crc32c_msgr_conn;
+
+/* kick(arg): a queued receive CRC or a held footer's CRC completed -- the
+ * messenger queues the connection's work (queue_con, messenger.c).
+ * release(msg): the adapter no longer references msg (reset or destroy),
+ * the messenger drops its reference (ceph_msg_put). */
+typedef void (*crc32c_msgr_kick_fn)(void *arg);
+typedef void (*crc32c_msgr_release_fn)(void *msg);
+
+/* A connection's adapter on async context `a` (shared by many connections;
+ * results complete in submission order per context).  max_pending bounds
+ * the receive queue (backpressure: rx_queue returns -EAGAIN when full). */
+struct crc32c_msgr_conn *crc32c_msgr_conn_create(struct crc32c_async *a, unsigned int max_pending,
+						 crc32c_msgr_kick_fn kick, void *kick_arg,
+						 crc32c_msgr_release_fn release);
+
+/* Fault / reconnect (con_fault, reset_connection): every queued receive
+ * message is released (now, or when its in-flight CRC completes); send
+ * entries are kept (a resent message reuses its CRC: the bytes are the same). */
+void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c);
+
+/* Reset, release the send entries too, free the adapter. */
+void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c);
+
+/* RECEIVE, at the footer (read_partial_message :2816): queue msg, whose data
+ * section is data[0, len).  check != 0 (do_datacrc and the footer has no
+ * CEPH_MSG_FOOTER_NOCRC flag): crc32c(0, data, len) is computed on the GPU
+ * and compared with footer_crc; otherwise the message is ready at once.  The
+ * messenger must not modify or free data until msg is returned by rx_next or
+ * released.  0, -EAGAIN (queue full: stop reading, dispatch first), or < 0. */
+int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data, unsigned int len, int check,
+			 uint32_t footer_crc);
+
+/* The queue head, in arrival order:
+ *   1        *msg verified (or unchecked); *crc = its data CRC (0 unchecked):
+ *            bump in_seq and dispatch it;
+ *   0        head not verified yet, or queue empty;
+ *   -EBADMSG *msg's data CRC differs from its footer (*crc = computed):
+ *            fault the connection ("bad crc", messenger.c:3137-3139).
+ * A message returned with 1 or -EBADMSG is no longer the adapter's. */
+int crc32c_msgr_rx_next(struct crc32c_msgr_conn *c, void **msg, uint32_t *crc);
+
+/* Messages queued and not yet returned. */
+unsigned int crc32c_msgr_rx_pending(const struct crc32c_msgr_conn *c);
+
+/* SEND: submit crc32c(seed, data, len) of outgoing msg (prepare_write_message;
+ * seed = footer.data_crc, 0 for a new message).  A msg that already has an
+ * entry (resend after a fault) keeps it: 0 without new work. */
+int crc32c_msgr_tx_submit(struct crc32c_msgr_conn *c, void *msg, const void *data, unsigned int len, uint32_t seed);
+
+/* SEND without a data pass: msg's data CRC is already known (REPOP fan-out:
+ * the verified request CRC, or crc32c_concat() of segment CRCs). */
+int crc32c_msgr_tx_known(struct crc32c_msgr_conn *c, void *msg, uint32_t crc);
+
+/* At the end of msg's data (write_partial_message_data :1793): 1 and *crc
+ * when ready (the entry is consumed), 0 when still running (hold the footer:
+ * kick() fires on completion), -ENOENT no entry for msg. */
+int crc32c_msgr_tx_footer(struct crc32c_msgr_conn *c, void *msg, uint32_t *crc);
+
+/* Counters of this adapter (all connections of the process). */
+struct crc32c_msgr_stats {
+	uint64_t rx_submitted, rx_unchecked, rx_verified, rx_bad, rx_released;
+	uint64_t tx_submitted, tx_known, tx_held, tx_released; /* held: footers that had to wait */
+};
+void crc32c_msgr_get_stats(struct crc32c_msgr_stats *st);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PECH_CRC32C_MSGR_H */

@@ -74,6 +74,21 @@ SIGNATURES = {
     "crc32c_concat": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                         ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint]),
     "crc32c_version": (ctypes.c_char_p, []),
+    # include/pech_crc32c_msgr.h (callbacks as plain pointers: driven from C, tests/c/msgr_conn_sim.c)
+    "crc32c_msgr_conn_create": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
+    "crc32c_msgr_conn_reset": (None, [ctypes.c_void_p]),
+    "crc32c_msgr_conn_destroy": (None, [ctypes.c_void_p]),
+    "crc32c_msgr_rx_queue": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint,
+                                            ctypes.c_int, ctypes.c_uint32]),
+    "crc32c_msgr_rx_next": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_uint32)]),
+    "crc32c_msgr_rx_pending": (ctypes.c_uint, [ctypes.c_void_p]),
+    "crc32c_msgr_tx_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint,
+                                             ctypes.c_uint32]),
+    "crc32c_msgr_tx_known": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
+    "crc32c_msgr_tx_footer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "crc32c_msgr_get_stats": (None, [ctypes.c_void_p]),
 }
 
 

@@ -1,0 +1,707 @@
+/*
+ * msgr_conn_sim.c -- TEST PROGRAM: pech's messenger connection state machine
+ * on the messenger adapter (include/pech_crc32c_msgr.h) and the async layer,
+ * in pech's dialect (gnu89 C, one OS thread, epoll loop).  Links the test
+ * oracle for expected values only.
+ *
+ * Plays out (file:line in /root/reference/src/ceph):
+ *   two clients -> one primary OSD -> two replicas, one connection each way.
+ *   SEND (write_partial_message_data, messenger.c:1748-1803): the data CRC is
+ *     submitted when a message is prepared (prepare_write_message :1345);
+ *     the data goes on the wire; at the footer the connection asks
+ *     crc32c_msgr_tx_footer() and HOLDS the footer (and every later message)
+ *     until the CRC is ready -- kicked by the adapter.  Every footer is
+ *     checked against the reference per-piece chain (oracle_crc32c_pieces).
+ *   RECEIVE (read_partial_message :2691-2851, process_message :2858): at the
+ *     footer the message is detached into the verify queue
+ *     (crc32c_msgr_rx_queue) and reading goes on; the seq check (:2737-2770)
+ *     runs against the RECEIVED count, while in_seq -- the value acks carry
+ *     (prepare_write_ack :1444) -- advances only in crc32c_msgr_rx_next, in
+ *     arrival order.  A queue-full -EAGAIN stops reading (backpressure).
+ *   FAULTS: some transmissions are corrupted on the wire after the sender
+ *     computed its footer.  The receiver must report -EBADMSG at that
+ *     message, fault the connection (reset: the queue is released, frames
+ *     in flight dropped), and the sender resends everything unacked from
+ *     in_seq + 1; duplicates are discarded by seq.  No corrupted payload is
+ *     ever dispatched, none is acked, every message is dispatched once, in
+ *     order.
+ *   REPOP (osd_server.c:1119 nested cursors, :1972 per replica): a write
+ *     whose ops all forward their data reuses the primary's verified CRC for
+ *     every replica (crc32c_msgr_tx_known: no data pass); a write that
+ *     forwards a subset of its ops gets one GPU CRC per forwarded segment
+ *     (async) and the REPOP footer is crc32c_concat() of them -- once for
+ *     both replicas.  Replicas verify through their own adapters.
+ *   GATES (libceph.h:36-37): mode "nocrc" runs with CEPH_OPT_NO_DATA_CRC --
+ *     footers carry CEPH_MSG_FOOTER_NOCRC, the adapter never submits -- and
+ *     header CRCs (do_hdrcrc) always use the drop-in crc32c() (host route).
+ * Usage: msgr_conn_sim [crc|nocrc] [messages per client] [corrupt every k]
+ * Exit 0 iff every invariant held; prints one summary line.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/epoll.h>
+#include <time.h>
+
+#include "pech_crc32c_msgr.h"
+
+uint32_t oracle_crc32c(uint32_t crc, const void *data, unsigned int length);
+uint32_t oracle_crc32c_pieces(uint32_t crc, const void *data, size_t length, unsigned int piece);
+
+#define MAX_SEGS 3
+#define HDR_LEN 49 /* offsetof(struct ceph_msg_header, crc), msgr.h:143-160 */
+
+enum { T_WRITE, T_REPOP };
+
+struct smsg {
+	int type, client, id;
+	unsigned char *data;
+	unsigned int len, nseg, seg[MAX_SEGS], fwd_mask; /* fwd_mask: ops whose data a REPOP forwards */
+	unsigned int order;                            /* pages order, ~0u: malloc */
+	uint32_t want;                                 /* oracle CRC of data (the test's truth) */
+	unsigned char hdr[HDR_LEN];
+	int refs;
+	/* primary-side REPOP construction for subset writes */
+	uint32_t segcrc[MAX_SEGS];
+	unsigned int segs_done, segs_needed;
+};
+
+struct frame {
+	struct frame *next;
+	struct smsg *src; /* the sender's message (for bookkeeping only) */
+	unsigned long long seq;
+	unsigned char *buf; /* receiver's copy (alloc_msg: pinned pages or malloc) */
+	unsigned int len, order;
+	uint32_t footer_crc, hdr_crc;
+	int nocrc, footer_ready, corrupt;
+};
+
+struct rx_msg { /* what the receiver's messenger holds per received message */
+	struct frame *f;
+};
+
+struct sconn {
+	const char *name;
+	struct sconn *peer; /* the other end */
+	struct crc32c_msgr_conn *ad;
+	int kicked;
+	/* send side */
+	struct smsg **outq;
+	unsigned long long *outq_seq;
+	unsigned int outq_n, outq_cap;
+	struct smsg **sent;
+	unsigned long long *sent_seq;
+	unsigned int sent_n, sent_cap;
+	unsigned long long out_seq;
+	struct smsg *holding; /* footer held for this message */
+	unsigned long long holding_seq;
+	struct frame *hold_frame;
+	/* receive side */
+	struct frame *wire_head, *wire_tail; /* frames from peer */
+	unsigned long long in_seq, in_seq_rcvd;
+	unsigned int dispatched, faults, dups;
+	int role; /* 0 client, 1 primary-in, 2 primary-out, 3 replica-in */
+	int replica;
+};
+
+static int do_datacrc = 1;
+static unsigned int corrupt_every = 7, nr_corrupted, nr_detected, nr_errors;
+static unsigned int dispatched_writes[2], dispatched_repops[2], repops_expected;
+static int next_id[2];
+static struct crc32c_async *actx;
+static uint32_t xs = 0x2545F491u;
+
+#define FAIL(...)                                  \
+	do {                                       \
+		fprintf(stderr, "FAIL: " __VA_ARGS__); \
+		nr_errors++;                       \
+	} while (0)
+
+static unsigned int rnd(void)
+{
+	xs ^= xs << 13;
+	xs ^= xs >> 17;
+	xs ^= xs << 5;
+	return xs;
+}
+
+static unsigned int order_for(unsigned int len)
+{
+	unsigned int o = 0;
+
+	while ((CRC32C_PAGE_SIZE << o) < len)
+		o++;
+	return o;
+}
+
+static unsigned char *buf_alloc(unsigned int len, unsigned int *order, int pinned)
+{
+	if (pinned && len <= (CRC32C_PAGE_SIZE << 11)) {
+		*order = order_for(len);
+		return crc32c_pages_alloc(*order);
+	}
+	*order = ~0u;
+	return malloc(len ? len : 1);
+}
+
+static void buf_free(unsigned char *p, unsigned int order)
+{
+	if (order == ~0u)
+		free(p);
+	else
+		crc32c_pages_free(p, order);
+}
+
+static void msg_put(struct smsg *m)
+{
+	if (--m->refs)
+		return;
+	buf_free(m->data, m->order);
+	free(m);
+}
+
+static void push(struct smsg ***arr, unsigned long long **seqs, unsigned int *n, unsigned int *cap, struct smsg *m,
+		 unsigned long long seq)
+{
+	if (*n == *cap) {
+		*cap = *cap ? *cap * 2 : 64;
+		*arr = realloc(*arr, *cap * sizeof(**arr));
+		*seqs = realloc(*seqs, *cap * sizeof(**seqs));
+	}
+	(*arr)[*n] = m;
+	(*seqs)[*n] = seq;
+	(*n)++;
+}
+
+/* ceph_con_send(): queue with the next out_seq (messenger.c:1377-1379) */
+static void con_send(struct sconn *c, struct smsg *m)
+{
+	m->refs++;
+	push(&c->outq, &c->outq_seq, &c->outq_n, &c->outq_cap, m, ++c->out_seq);
+}
+
+static void hdr_fill(struct smsg *m)
+{
+	unsigned int i;
+
+	for (i = 0; i < HDR_LEN; i++)
+		m->hdr[i] = (unsigned char)rnd();
+	m->hdr[0] = (unsigned char)m->type;
+}
+
+static struct smsg *new_write(int client)
+{
+	static const unsigned int sizes[] = {0, 1, 100, 4096, 4097, 65536, 131072 + 7, 1 << 20, (4 << 20) + 3};
+	struct smsg *m = calloc(1, sizeof(*m));
+	unsigned int i, left;
+
+	m->type = T_WRITE;
+	m->client = client;
+	m->id = next_id[client]++;
+	m->len = sizes[rnd() % (sizeof(sizes) / sizeof(sizes[0]))];
+	m->data = buf_alloc(m->len, &m->order, rnd() % 3 != 0);
+	for (i = 0; i < m->len; i++)
+		m->data[i] = (unsigned char)rnd();
+	m->want = oracle_crc32c(0, m->data, m->len);
+	/* 1..3 ops partition the data (each op's indata in order) */
+	m->nseg = m->len >= 3 ? 1 + rnd() % MAX_SEGS : 1;
+	left = m->len;
+	for (i = 0; i < m->nseg; i++) {
+		m->seg[i] = i + 1 == m->nseg ? left : rnd() % (left / 2 + 1);
+		left -= m->seg[i];
+	}
+	m->fwd_mask = (m->nseg > 1 && rnd() % 3 == 0) ? ((1u << m->nseg) - 1) & ~(1u << (rnd() % m->nseg))
+						    : (1u << m->nseg) - 1;
+	if (!m->fwd_mask)
+		m->fwd_mask = 1;
+	hdr_fill(m);
+	m->refs = 1;
+	return m;
+}
+
+/* ---- send side ------------------------------------------------------- */
+
+static void wire_push(struct sconn *to, struct frame *f)
+{
+	f->next = NULL;
+	if (to->wire_tail)
+		to->wire_tail->next = f;
+	else
+		to->wire_head = f;
+	to->wire_tail = f;
+}
+
+/* the footer of c->holding: once the CRC is ready */
+static int try_footer(struct sconn *c)
+{
+	uint32_t crc = 0;
+	struct frame *f = c->hold_frame;
+	struct smsg *m = c->holding;
+	int rc;
+
+	if (!m)
+		return 1;
+	if (do_datacrc) {
+		rc = crc32c_msgr_tx_footer(c->ad, m, &crc);
+		if (rc == 0)
+			return 0; /* hold: kicked when the CRC lands */
+		if (rc < 0) {
+			FAIL("%s tx_footer %d\n", c->name, rc);
+			return -1;
+		}
+		/* a6: the footer equals the reference's per-piece chain */
+		if (crc != oracle_crc32c_pieces(0, m->data, m->len, 4096))
+			FAIL("%s send footer %08x != reference %08x (len %u)\n", c->name, crc,
+			     oracle_crc32c_pieces(0, m->data, m->len, 4096), m->len);
+		f->footer_crc = crc;
+	} else {
+		f->nocrc = 1; /* CEPH_MSG_FOOTER_NOCRC (messenger.c:1798) */
+	}
+	f->footer_ready = 1;
+	push(&c->sent, &c->sent_seq, &c->sent_n, &c->sent_cap, m, c->holding_seq);
+	c->holding = NULL;
+	c->hold_frame = NULL;
+	return 1;
+}
+
+static int try_write(struct sconn *c)
+{
+	int progress = 0;
+
+	while (!c->holding && c->outq_n) {
+		struct smsg *m = c->outq[0];
+		unsigned long long seq = c->outq_seq[0];
+		struct frame *f = calloc(1, sizeof(*f));
+
+		memmove(c->outq, c->outq + 1, (c->outq_n - 1) * sizeof(*c->outq));
+		memmove(c->outq_seq, c->outq_seq + 1, (c->outq_n - 1) * sizeof(*c->outq_seq));
+		c->outq_n--;
+		/* prepare_write_message: header CRC on the host (drop-in), data CRC submitted */
+		f->hdr_crc = crc32c(0, m->hdr, HDR_LEN);
+		if (do_datacrc && crc32c_msgr_tx_submit(c->ad, m, m->data, m->len, 0))
+			FAIL("%s tx_submit\n", c->name);
+		/* the data on the wire: the receiver's buffer (alloc_msg) */
+		f->src = m;
+		f->seq = seq;
+		f->len = m->len;
+		f->buf = buf_alloc(m->len, &f->order, rnd() % 3 != 0);
+		memcpy(f->buf, m->data, m->len);
+		if (corrupt_every && do_datacrc && m->len && rnd() % corrupt_every == 0) {
+			f->corrupt = 1; /* flipped after the sender's CRC: must be caught */
+			f->buf[rnd() % m->len] ^= (unsigned char)(1u << (rnd() % 8));
+			nr_corrupted++;
+		}
+		wire_push(c->peer, f);
+		c->holding = m;
+		c->holding_seq = seq;
+		c->hold_frame = f;
+		progress = 1;
+		if (try_footer(c) <= 0)
+			break;
+	}
+	return progress;
+}
+
+/* ---- receive side ----------------------------------------------------- */
+
+static void rx_release(void *p)
+{
+	struct rx_msg *r = p;
+
+	buf_free(r->f->buf, r->f->order);
+	free(r->f);
+	free(r);
+}
+
+static void kick(void *arg)
+{
+	((struct sconn *)arg)->kicked = 1;
+}
+
+static int try_read(struct sconn *c)
+{
+	int progress = 0;
+
+	while (c->wire_head && c->wire_head->footer_ready) {
+		struct frame *f = c->wire_head;
+		struct rx_msg *r;
+		int rc;
+
+		if (f->seq <= c->in_seq_rcvd) { /* duplicate of a received message (messenger.c:2737) */
+			c->wire_head = f->next;
+			if (!c->wire_head)
+				c->wire_tail = NULL;
+			buf_free(f->buf, f->order);
+			free(f);
+			c->dups++;
+			continue;
+		}
+		if (f->seq != c->in_seq_rcvd + 1) {
+			FAIL("%s seq %llu after %llu: a message was lost\n", c->name, f->seq, c->in_seq_rcvd);
+			return -1;
+		}
+		if (crc32c(0, f->src->hdr, HDR_LEN) != f->hdr_crc) /* do_hdrcrc: host route */
+			FAIL("%s header crc\n", c->name);
+		r = calloc(1, sizeof(*r));
+		r->f = f;
+		rc = crc32c_msgr_rx_queue(c->ad, r, f->buf, f->len, do_datacrc && !f->nocrc, f->footer_crc);
+		if (rc == -EAGAIN) {
+			free(r);
+			break; /* backpressure: leave it on the wire */
+		}
+		if (rc) {
+			FAIL("%s rx_queue %d\n", c->name, rc);
+			free(r);
+			return -1;
+		}
+		c->wire_head = f->next;
+		if (!c->wire_head)
+			c->wire_tail = NULL;
+		c->in_seq_rcvd++;
+		progress = 1;
+	}
+	return progress;
+}
+
+static struct sconn conns[4]; /* send sides: client0, client1, primary->r0, primary->r1 */
+static struct sconn *cli[2], *pin[2], *pout[2], *rin[2];
+
+static void fault(struct sconn *c)
+{
+	struct sconn *s = c->peer;
+	struct frame *f, *n;
+	unsigned int i;
+
+	c->faults++;
+	crc32c_msgr_conn_reset(c->ad); /* queued messages released (after in-flight CRCs land) */
+	c->in_seq_rcvd = c->in_seq;    /* only dispatched messages count as received */
+	for (f = c->wire_head; f; f = n) {
+		n = f->next;
+		buf_free(f->buf, f->order);
+		free(f);
+	}
+	c->wire_head = c->wire_tail = NULL;
+	/* the peer reconnects: everything unacked goes out again with its seq */
+	if (s->holding) {
+		push(&s->sent, &s->sent_seq, &s->sent_n, &s->sent_cap, s->holding, s->holding_seq);
+		s->holding = NULL;
+		s->hold_frame = NULL; /* its frame was on the dropped wire */
+	}
+	for (i = 0; i < s->outq_n; i++)
+		push(&s->sent, &s->sent_seq, &s->sent_n, &s->sent_cap, s->outq[i], s->outq_seq[i]);
+	s->outq_n = 0;
+	/* the peer only knows what was ACKED: it resends everything else, so
+	 * messages dispatched but not yet acked come again as duplicates */
+	for (i = 0; i < s->sent_n; i++)
+		push(&s->outq, &s->outq_seq, &s->outq_n, &s->outq_cap, s->sent[i], s->sent_seq[i]);
+	s->sent_n = 0;
+}
+
+/* prepare_write_ack (messenger.c:1444): the peer drops what is acked */
+static void ack(struct sconn *c)
+{
+	struct sconn *s = c->peer;
+	unsigned int i, k = 0;
+
+	for (i = 0; i < s->sent_n; i++) {
+		if (s->sent_seq[i] <= c->in_seq) {
+			msg_put(s->sent[i]);
+		} else {
+			s->sent[k] = s->sent[i];
+			s->sent_seq[k++] = s->sent_seq[i];
+		}
+	}
+	s->sent_n = k;
+}
+
+static void repop_seg_done(void *arg, uint32_t crc, int err);
+
+static void send_repops(struct smsg *w, uint32_t crc, int known)
+{
+	int r;
+
+	for (r = 0; r < 2; r++) {
+		struct smsg *rep = calloc(1, sizeof(*rep));
+		unsigned int i, off = 0, o = 0;
+
+		rep->type = T_REPOP;
+		rep->client = w->client;
+		rep->id = w->id;
+		/* data: the forwarded ops' segments, in op order (nested cursors) */
+		for (i = 0; i < w->nseg; i++)
+			if (w->fwd_mask & (1u << i))
+				rep->len += w->seg[i];
+		rep->data = buf_alloc(rep->len, &rep->order, 1);
+		for (i = 0; i < w->nseg; off += w->seg[i], i++)
+			if (w->fwd_mask & (1u << i)) {
+				memcpy(rep->data + o, w->data + off, w->seg[i]);
+				o += w->seg[i];
+			}
+		rep->want = oracle_crc32c(0, rep->data, rep->len);
+		hdr_fill(rep);
+		rep->refs = 1;
+		if (known && do_datacrc) {
+			/* f3: the CRC is known without a data pass; the same for every replica */
+			if (crc != rep->want)
+				FAIL("repop crc %08x != reference %08x (client %d id %d)\n", crc, rep->want, w->client,
+				     w->id);
+			crc32c_msgr_tx_known(pout[r]->ad, rep, crc);
+		}
+		con_send(pout[r], rep);
+		msg_put(rep);
+		repops_expected++;
+	}
+}
+
+static void repop_seg_done(void *arg, uint32_t crc, int err)
+{
+	struct smsg *w = arg;
+	unsigned int k = w->segs_done++;
+	uint64_t lens[MAX_SEGS];
+	uint32_t crcs[MAX_SEGS];
+	unsigned int i, n = 0;
+
+	if (err)
+		FAIL("segment crc err %d\n", err);
+	w->segcrc[k] = crc;
+	if (w->segs_done < w->segs_needed)
+		return;
+	for (i = 0; i < w->nseg; i++)
+		if (w->fwd_mask & (1u << i)) {
+			lens[n] = w->seg[i];
+			crcs[n] = w->segcrc[n];
+			n++;
+		}
+	send_repops(w, crc32c_concat(0, crcs, lens, n), 1);
+	msg_put(w);
+}
+
+/* the OSD's dispatch of a verified client write (osds_dispatch -> REPOP) */
+static void osd_write(struct smsg *w, uint32_t crc)
+{
+	unsigned int i, off = 0;
+
+	if (!do_datacrc || w->fwd_mask == (1u << w->nseg) - 1) {
+		send_repops(w, crc, 1); /* whole request data forwarded: its verified CRC */
+		return;
+	}
+	/* a subset: one GPU CRC per forwarded op segment, then crc32c_concat */
+	w->refs++;
+	w->segs_needed = 0;
+	for (i = 0; i < w->nseg; i++)
+		if (w->fwd_mask & (1u << i))
+			w->segs_needed++;
+	for (i = 0; i < w->nseg; off += w->seg[i], i++)
+		if ((w->fwd_mask & (1u << i)) && crc32c_async_submit(actx, w->data + off, w->seg[i], 0, repop_seg_done, w))
+			FAIL("segment submit\n");
+}
+
+static int dispatch(struct sconn *c)
+{
+	int progress = 0;
+
+	for (;;) {
+		void *p = NULL;
+		uint32_t crc = 0;
+		struct rx_msg *r;
+		struct frame *f;
+		int rc = crc32c_msgr_rx_next(c->ad, &p, &crc);
+
+		if (rc == 0)
+			break;
+		r = p;
+		f = r->f;
+		if (rc == -EBADMSG) {
+			if (!f->corrupt)
+				FAIL("%s -EBADMSG on an intact message\n", c->name);
+			nr_detected++;
+			rx_release(r);
+			fault(c);
+			return 1;
+		}
+		if (rc != 1) {
+			FAIL("%s rx_next %d\n", c->name, rc);
+			return -1;
+		}
+		/* process_message: in_seq advances only now, in order */
+		c->in_seq++;
+		if (f->seq != c->in_seq)
+			FAIL("%s dispatched seq %llu as #%llu\n", c->name, f->seq, c->in_seq);
+		if (f->corrupt && do_datacrc)
+			FAIL("%s dispatched a corrupted payload\n", c->name);
+		if (oracle_crc32c(0, f->buf, f->len) != f->src->want)
+			FAIL("%s dispatched wrong bytes\n", c->name);
+		if (do_datacrc && crc != f->src->want)
+			FAIL("%s verified crc %08x != %08x\n", c->name, crc, f->src->want);
+		c->dispatched++;
+		if (c->role == 1) {
+			struct smsg *w = f->src;
+
+			if (w->id != (int)dispatched_writes[w->client])
+				FAIL("client %d write %d dispatched out of order\n", w->client, w->id);
+			dispatched_writes[w->client]++;
+			w->refs++; /* the OSD keeps the request while it replicates (osd_server.c:1962) */
+			osd_write(w, crc);
+			msg_put(w);
+		} else {
+			dispatched_repops[c->replica]++;
+		}
+		rx_release(r);
+		progress = 1;
+	}
+	return progress;
+}
+
+static unsigned int tx_releases;
+
+/* send-side entries come back here only at destroy (the queues hold the refs) */
+static void tx_release(void *msg)
+{
+	(void)msg;
+	tx_releases++;
+}
+
+static struct sconn *mk(struct sconn *c, const char *name, int role)
+{
+	c->name = name;
+	c->role = role;
+	c->ad = crc32c_msgr_conn_create(actx, 24, kick, c, (role == 0 || role == 2) ? tx_release : rx_release);
+	return c;
+}
+
+static double now_s(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+int main(int argc, char **argv)
+{
+	const unsigned int n = argc > 2 ? (unsigned int)atoi(argv[2]) : 120;
+	struct crc32c_msgr_stats st;
+	struct crc32c_stats ds;
+	struct epoll_event ev;
+	unsigned int i, sent[2] = {0, 0};
+	double t0;
+	int ep, k;
+
+	do_datacrc = !(argc > 1 && !strcmp(argv[1], "nocrc"));
+	if (argc > 3)
+		corrupt_every = (unsigned int)atoi(argv[3]);
+	actx = crc32c_async_create(CRC32C_ASYNC_DEFAULT);
+	if (!actx) {
+		fprintf(stderr, "crc32c_async_create: %s\n", crc32c_last_error());
+		return 2;
+	}
+	ep = epoll_create1(0);
+	memset(&ev, 0, sizeof(ev));
+	ev.events = EPOLLIN;
+	epoll_ctl(ep, EPOLL_CTL_ADD, crc32c_async_fd(actx), &ev);
+	/* send sides and receive sides of each link */
+	cli[0] = mk(&conns[0], "client0", 0);
+	cli[1] = mk(&conns[1], "client1", 0);
+	pout[0] = mk(&conns[2], "primary->r0", 2);
+	pout[1] = mk(&conns[3], "primary->r1", 2);
+	pin[0] = calloc(1, sizeof(struct sconn));
+	pin[1] = calloc(1, sizeof(struct sconn));
+	rin[0] = calloc(1, sizeof(struct sconn));
+	rin[1] = calloc(1, sizeof(struct sconn));
+	mk(pin[0], "primary<-client0", 1);
+	mk(pin[1], "primary<-client1", 1);
+	mk(rin[0], "r0<-primary", 3);
+	mk(rin[1], "r1<-primary", 3);
+	rin[0]->replica = 0;
+	rin[1]->replica = 1;
+	for (k = 0; k < 2; k++) {
+		cli[k]->peer = pin[k];
+		pin[k]->peer = cli[k];
+		pout[k]->peer = rin[k];
+		rin[k]->peer = pout[k];
+	}
+	t0 = now_s();
+	for (;;) {
+		int progress = 0;
+		struct sconn *all[8] = {cli[0], cli[1], pout[0], pout[1], pin[0], pin[1], rin[0], rin[1]};
+
+		/* clients submit a few writes at a time */
+		for (k = 0; k < 2; k++)
+			for (i = 0; i < 3 && sent[k] < n; i++, sent[k]++) {
+				struct smsg *m = new_write(k);
+
+				con_send(cli[k], m);
+				msg_put(m);
+				progress = 1;
+			}
+		for (i = 0; i < 8; i++) {
+			struct sconn *c = all[i];
+
+			c->kicked = 0;
+			if (c->holding && try_footer(c) > 0)
+				progress = 1;
+			if (try_write(c) > 0)
+				progress = 1;
+			if (try_read(c) > 0)
+				progress = 1;
+		}
+		if (crc32c_async_flush(actx))
+			FAIL("flush: %s\n", crc32c_last_error());
+		for (i = 0; i < 8; i++) {
+			if (dispatch(all[i]) > 0)
+				progress = 1;
+			if (all[i]->in_seq && rnd() % 2)
+				ack(all[i]);
+		}
+		if (dispatched_writes[0] == n && dispatched_writes[1] == n &&
+		    dispatched_repops[0] + dispatched_repops[1] == repops_expected && !crc32c_async_pending(actx))
+			break;
+		if (nr_errors > 20 || now_s() - t0 > 60) {
+			FAIL("stuck: writes %u/%u %u/%u repops %u+%u/%u pending %u\n", dispatched_writes[0], n,
+			     dispatched_writes[1], n, dispatched_repops[0], dispatched_repops[1], repops_expected,
+			     crc32c_async_pending(actx));
+			break;
+		}
+		if (epoll_wait(ep, &ev, 1, progress ? 0 : 20) > 0 || crc32c_async_pending(actx))
+			if (crc32c_async_complete(actx) < 0)
+				FAIL("complete: %s\n", crc32c_last_error());
+	}
+	for (k = 0; k < 2; k++) {
+		ack(pin[k]);
+		ack(rin[k]);
+	}
+	crc32c_async_drain(actx);
+	crc32c_msgr_get_stats(&st);
+	crc32c_get_stats(&ds);
+	if (do_datacrc && nr_detected != nr_corrupted)
+		FAIL("corrupted %u, detected %u\n", nr_corrupted, nr_detected);
+	if (!do_datacrc && (st.rx_submitted || st.tx_submitted || st.rx_verified))
+		FAIL("NO_DATA_CRC: the adapter computed CRCs\n");
+	if (do_datacrc && st.rx_unchecked)
+		FAIL("data CRC on: %llu messages went unchecked\n", (unsigned long long)st.rx_unchecked);
+	if (ds.gpu_calls)
+		FAIL("header CRCs went to the GPU (%llu calls)\n", (unsigned long long)ds.gpu_calls);
+	for (k = 0; k < 4; k++)
+		crc32c_msgr_conn_destroy(conns[k].ad);
+	if (tx_releases)
+		FAIL("%u send entries were never consumed by a footer\n", tx_releases);
+	for (k = 0; k < 2; k++) {
+		crc32c_msgr_conn_destroy(pin[k]->ad);
+		crc32c_msgr_conn_destroy(rin[k]->ad);
+	}
+	crc32c_async_destroy(actx);
+	printf("msgr_conn_sim %s: writes %u+%u dispatched, repops %u+%u of %u, corrupted %u detected %u, faults %u, "
+	       "dups %u; adapter rx submitted %llu verified %llu bad %llu unchecked %llu released %llu, tx submitted "
+	       "%llu known %llu held %llu; drop-in host calls %llu; %u errors\n",
+	       do_datacrc ? "crc" : "nocrc", dispatched_writes[0], dispatched_writes[1], dispatched_repops[0],
+	       dispatched_repops[1], repops_expected, nr_corrupted, nr_detected,
+	       pin[0]->faults + pin[1]->faults + rin[0]->faults + rin[1]->faults,
+	       pin[0]->dups + pin[1]->dups + rin[0]->dups + rin[1]->dups, (unsigned long long)st.rx_submitted,
+	       (unsigned long long)st.rx_verified, (unsigned long long)st.rx_bad, (unsigned long long)st.rx_unchecked,
+	       (unsigned long long)st.rx_released, (unsigned long long)st.tx_submitted,
+	       (unsigned long long)st.tx_known, (unsigned long long)st.tx_held, (unsigned long long)ds.cpu_calls,
+	       nr_errors);
+	return nr_errors ? 1 : 0;
+}

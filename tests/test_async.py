@@ -147,3 +147,26 @@ def test_msgr_sim_event_loop(zerocopy, contexts):
     r = subprocess.run([exe, "200", zerocopy, contexts], capture_output=True, timeout=120)
     assert r.returncode == 0, (r.stdout.decode(), r.stderr.decode())
     assert b"0 bad" in r.stdout
+
+
+def test_msgr_conn_sim_builds_as_pech_c():
+    r = subprocess.run(["make", "-s", "-C", REPO, "build/msgr_conn_sim"], capture_output=True)
+    assert r.returncode == 0, r.stderr.decode()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,corrupt", [("crc", "7"), ("crc", "0"), ("nocrc", "0")])
+def test_msgr_connection_state_machine(mode, corrupt):
+    # tests/c/msgr_conn_sim.c: send-side held footers (a6), receive verify
+    # queue with in-order dispatch and acks only after verification (a5, f1),
+    # corruption -> -EBADMSG -> fault -> resend (no corrupted dispatch),
+    # REPOP footers by CRC reuse / crc32c_concat of per-op GPU CRCs (f3),
+    # NO_DATA_CRC / header-CRC gates (a10); every footer vs the reference chain
+    exe = os.path.join(REPO, "build", "msgr_conn_sim")
+    assert os.path.exists(exe), "build/msgr_conn_sim is built by `make`"
+    r = subprocess.run([exe, mode, "150", corrupt], capture_output=True, timeout=240)
+    out = r.stdout.decode() + r.stderr.decode()
+    assert r.returncode == 0, out[-4000:]
+    assert " 0 errors" in out
+    if mode == "crc" and corrupt != "0":
+        assert "corrupted 0 " not in out  # the run did inject and catch corruption

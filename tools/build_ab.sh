@@ -6,7 +6,7 @@
 # revision (e.g. the previous release) for before/after comparisons.
 set -e
 cd "$(dirname "$0")/.."
-make -s build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o
+make -s build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o build/crc32c_msgr.o
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function"
 for spec in "$@"; do
@@ -16,7 +16,7 @@ for spec in "$@"; do
     git show "$arg":pech_amd/csrc/crc32c_kernels.hip > build/rev_$arg/crc32c_kernels.hip
     $HIPCC $FLAGS -Ipech_amd/csrc -c build/rev_$arg/crc32c_kernels.hip -o build/k_rev_$arg.o
     $HIPCC $FLAGS -shared -o build/lib_$arg.so build/k_rev_$arg.o build/crc32c_api.o build/crc32c_async.o \
-      build/crc32c_cpu.o
+      build/crc32c_cpu.o build/crc32c_msgr.o
     echo "build/lib_$arg.so"
   else
     make -s variant V="$name" D="$arg"
