@@ -13,7 +13,7 @@ HOST_OBJ = build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o build/crc3
 OBJ = build/crc32c_kernels.o $(HOST_OBJ)
 
 all: $(LIB) oracle build/msgr_sim build/msgr_conn_sim build/dropin_kat build/coro_stack build/dropin_bench \
-     build/lib_dbg.so
+     build/lib_dbg.so build/hbm_probe build/sched_probe
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -100,3 +100,12 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all asm variant oracle clean
+
+# GPU-box probes (not product code): HBM read shapes, work-distribution schedules
+build/hbm_probe: tools/hbm_probe.hip
+	@mkdir -p build
+	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@
+
+build/sched_probe: tools/sched_probe.hip
+	@mkdir -p build
+	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@

@@ -84,6 +84,12 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
     ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
+    ap.add_argument("--single-thread", action="store_true",
+                    help="pech's model: ONE process drives --gpus devices (hipSetDevice + crc32c_dev_batch_ws_async "
+                         "per device, own streams and workspaces), instead of one process per GPU")
+    ap.add_argument("--devices", default=None,
+                    help="with --single-thread: comma-separated device list (default 0..gpus-1); a repeated id "
+                         "puts several shards on one GPU (rehearsal on a 1-GPU box)")
     return ap.parse_args()
 
 
@@ -109,7 +115,13 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
+    if args.single_thread:
+        if world > 1:
+            raise SystemExit("--single-thread is one process: do not launch it under torchrun")
+        devids = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    else:
+        devids = [local]
+    dev = torch.device("cuda", devids[0])
     torch.cuda.set_device(dev)
 
     import pech_amd as P
@@ -122,55 +134,76 @@ def main():
     n = len(sizes)
     batch_bytes = int(sizes.sum())
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
-
-    # resident inputs: `rotate` distinct batches of random bytes + descriptors
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1000 + rank)
-    bufs, descs = [], []
-    for r in range(rotate):
-        b = torch.randint(0, 256, (batch_bytes,), dtype=torch.uint8, device=dev, generator=gen)
-        bufs.append(b)
-        descs.append(P.make_descs(b.data_ptr() + offs, sizes, device=dev))
-    outs = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(rotate)]
-    dsts = []
-    if args.op == "copy":  # a destination buffer per rotating batch, same layout
-        for r in range(rotate):
-            d = torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
-            dsts.append((d, torch.from_numpy((d.data_ptr() + offs).astype(np.int64)).to(dev)))
-    assert _lib.lib().crc32c_dev_reserve(n) == 0
     maxs = max(1, args.streams)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(maxs - 1)]
-    wsb = P.workspace_bytes(n)
-    wss = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(maxs)]
+
+    class Shard:
+        """One device's batches: `rotate` distinct resident batches of random
+        bytes + descriptors, outputs, streams and a workspace per stream."""
+
+        def __init__(self, d, seed):
+            self.dev = torch.device("cuda", d)
+            with torch.cuda.device(self.dev):
+                gen = torch.Generator(device=self.dev)
+                gen.manual_seed(seed)
+                self.bufs, self.descs = [], []
+                for r in range(rotate):
+                    b = torch.randint(0, 256, (batch_bytes,), dtype=torch.uint8, device=self.dev, generator=gen)
+                    self.bufs.append(b)
+                    self.descs.append(P.make_descs(b.data_ptr() + offs, sizes, device=self.dev))
+                self.outs = [torch.zeros(n, dtype=torch.int32, device=self.dev) for _ in range(rotate)]
+                self.dsts = []
+                if args.op == "copy":  # a destination buffer per rotating batch, same layout
+                    for r in range(rotate):
+                        dd = torch.empty(batch_bytes, dtype=torch.uint8, device=self.dev)
+                        self.dsts.append((dd, torch.from_numpy((dd.data_ptr() + offs).astype(np.int64)).to(self.dev)))
+                assert _lib.lib().crc32c_dev_reserve(n) == 0
+                self.streams = [torch.cuda.current_stream(self.dev) if not args.single_thread
+                                else torch.cuda.Stream(self.dev)] + \
+                               [torch.cuda.Stream(self.dev) for _ in range(maxs - 1)]
+                wsb = P.workspace_bytes(n)
+                self.wss = [torch.empty(wsb, dtype=torch.uint8, device=self.dev) for _ in range(maxs)]
+
+        def step(self, i, k):
+            with torch.cuda.device(self.dev):
+                if self.dsts:
+                    P.dev_copy_batch_ws_async(self.descs[i % rotate], self.dsts[i % rotate][1],
+                                              self.outs[i % rotate], self.wss[k], stream=self.streams[k])
+                else:
+                    P.dev_batch_ws_async(self.descs[i % rotate], self.outs[i % rotate], self.wss[k],
+                                         stream=self.streams[k])
+
+    shards = [Shard(d, 1000 + rank * 64 + j) for j, d in enumerate(devids)]
+    bufs, outs, dsts = shards[0].bufs, shards[0].outs, shards[0].dsts
+
+    def sync_all():
+        for d in sorted(set(devids)):
+            torch.cuda.synchronize(torch.device("cuda", d))
 
     def timed(nstreams, steps, warmup):
         """Warm-up, then `steps` batches bracketed by barrier + synchronize;
-        batch i on stream i % nstreams (own workspace).  A batch's output
-        buffer is only ever written from one stream, so steps never race.
-        Returns (elapsed seconds, max over ranks; per-launch main-kernel us)."""
+        batch i on stream i % nstreams (own workspace) of every shard.  A
+        batch's output buffer is only ever written from one stream, so steps
+        never race.  Returns (elapsed seconds, max over ranks; per-launch
+        main-kernel us)."""
         if rotate % nstreams:
             raise SystemExit(f"{nstreams} streams must divide the {rotate} rotating batches")
 
         def step(i):
-            k = i % nstreams
-            if dsts:
-                P.dev_copy_batch_ws_async(descs[i % rotate], dsts[i % rotate][1], outs[i % rotate], wss[k],
-                                          stream=streams[k])
-            else:
-                P.dev_batch_ws_async(descs[i % rotate], outs[i % rotate], wss[k], stream=streams[k])
+            for sh in shards:  # one host thread issues every device's batch, then the next
+                sh.step(i, i % nstreams)
 
         for i in range(warmup):
             step(i)
-        torch.cuda.synchronize(dev)
+        sync_all()
         P.timing(not args.no_kernel_events)
         P.timing_read()  # discard warm-up launches
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync_all()
         t0 = time.perf_counter()
         for i in range(steps):
             step(i)
-        torch.cuda.synchronize(dev)
+        sync_all()
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
@@ -195,7 +228,7 @@ def main():
     launches = len(samples)
     kernel_ms = float(samples.sum()) / 1e3
 
-    total_bytes = batch_bytes * args.steps * world
+    total_bytes = batch_bytes * args.steps * world * len(shards)
     value = total_bytes / elapsed / (1 << 30)
     avg_kernel_s = kernel_ms / 1e3 / max(launches, 1)
     # algorithmic HBM bytes per launch: each payload byte read once (+ written
@@ -208,17 +241,19 @@ def main():
     # MI355X_MICROARCH.md), used only when it was taken on this kernel build.
     traffic = None
     tag = args.config + ("-copy" if dsts else "")
-    pj = args.profile_json or os.path.join(REPO, "profiles", "r01", f"{tag}_traffic.json")
-    if os.path.exists(pj):
-        prof = json.load(open(pj))
-        if prof.get("kernel") == P.version():
-            traffic = prof.get("hbm_bytes_per_launch")
+    for pj in ([args.profile_json] if args.profile_json else
+               [os.path.join(REPO, "profiles", r, f"{tag}_traffic.json") for r in ("r02", "r01")]):
+        if os.path.exists(pj):
+            prof = json.load(open(pj))
+            if prof.get("kernel") == P.version():
+                traffic = prof.get("hbm_bytes_per_launch")
+                break
 
     line = {
         "metric": "CRC32C GiB/s on device-resident object buffers (4 KiB–4 MiB), 1/2/4/8 GPUs",
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": world * len(set(devids)),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -229,7 +264,9 @@ def main():
         "data": "synthetic (uniform random bytes, torch.randint on device), seed 0 per buffer",
         "config": {"workload": desc + ("; fused CRC + copy to a second buffer (read + write)" if dsts else ""),
                    "buffers_per_gpu": n, "bytes_per_gpu_per_step": batch_bytes,
-                   "parallelism": f"shard{world} (independent buffers per GPU, no collective)",
+                   "parallelism": (f"single-thread: one process drives {len(shards)} shard(s) on device(s) "
+                                   f"{','.join(map(str, devids))}, no collective" if args.single_thread else
+                                   f"shard{world} (independent buffers per GPU, no collective)"),
                    "streams": nstreams,
                    "kernel": P.version()},
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -242,7 +279,7 @@ def main():
         "serial": {"streams": 1, "value": round(total_bytes / serial_el / (1 << 30), 2), "unit": "GiB/s",
                    "ms_per_step": round(serial_el / args.steps * 1e3, 4)},
     }
-    if rank == 0 and world == 1 and not args.no_host_path and not dsts:
+    if rank == 0 and world == 1 and len(shards) == 1 and not args.no_host_path and not dsts:
         line["pcie_inclusive"] = host_path(args, bufs[0], offs, sizes, outs, P)
         line["dropin_crc32c"] = dropin_latency(P)
         # uniform payloads: the C adapter benchmark (no Python per submit);
@@ -252,8 +289,11 @@ def main():
             line["msgr_async"] = msgr_c_bench(args, int(sizes[0]), n)
         else:
             line["msgr_async"] = msgr_path(args, bufs[0], offs, sizes, outs, P) if n <= 4096 else None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not dsts:
+    if rank == 0 and world == 1 and len(shards) == 1 and not args.no_cpu_baseline and not dsts:
         line["cpu_baseline"] = cpu_baseline(args, bufs[0], offs, sizes, outs, rotate, P)
+
+    if len(shards) > 1:
+        line["shards_checked"] = shard_parity(shards, offs, sizes, rotate, P)
 
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -403,6 +443,27 @@ def msgr_c_bench(args, size, count):
             "path": f"C: crc32c_async_submit per {size}-byte payload from crc32c_pages memory, flush every 64, "
                     "drain via eventfd (build/msgr_sim bench); zerocopy: kernel reads pinned payloads below 1 MiB in place, larger ones DMA'd",
             "payloads": count, "passes": args.host_passes, "matches_oracle": True}
+
+
+def shard_parity(shards, offs, sizes, rotate, P):
+    """Single-thread multi-shard runs: every shard's last outputs for its
+    first and last buffers against the oracle (test infrastructure, outside
+    the timed region)."""
+    import torch
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+
+    for sh in shards:
+        torch.cuda.synchronize(sh.dev)
+        for r in range(rotate):
+            got = sh.outs[r].cpu().numpy().view(np.uint32)
+            for i in (0, len(sizes) - 1):
+                lo, hi = int(offs[i]), int(offs[i] + sizes[i])
+                want = O.crc(0, sh.bufs[r][lo:hi].cpu().numpy())
+                if int(got[i]) != want:
+                    raise SystemExit(f"PARITY FAILURE: shard on {sh.dev}, batch {r}, buffer {i}")
+    return len(shards)
 
 
 def cpu_baseline(args, buf0, offs, sizes, outs, rotate, P):

@@ -1,0 +1,35 @@
+"""bench.py's two multi-GPU drivers emit the same JSON schema (GPU box):
+torchrun's one process per GPU (here N=1) and pech's model, one host thread
+driving every device (--single-thread), including two shards on one GPU
+(--devices 0,0, the 1-GPU rehearsal of the loop)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ["--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--no-host-path"]
+
+
+def run(*extra):
+    r = subprocess.run([sys.executable, "bench.py", *COMMON, *extra], cwd=REPO, capture_output=True, timeout=240)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    return json.loads(r.stdout.decode().strip().splitlines()[-1])
+
+
+def test_single_thread_matches_process_per_gpu_schema():
+    a = run()
+    b = run("--single-thread", "--gpus", "1")
+    c = run("--single-thread", "--devices", "0,0")
+    assert set(a) == set(b) and set(a["roofline"]) == set(b["roofline"])
+    assert set(c) - set(a) == {"shards_checked"} and c["shards_checked"] == 2
+    assert a["n_gpus"] == b["n_gpus"] == c["n_gpus"] == 1
+    assert "single-thread" in b["config"]["parallelism"] and "single-thread" in c["config"]["parallelism"]
+    # same work on one GPU: the two drivers agree (the bench log records ~1-2 %)
+    assert abs(a["value"] - b["value"]) / a["value"] < 0.10, (a["value"], b["value"])
+    # two shards on one GPU share its HBM: about one GPU's rate in aggregate
+    assert 0.7 < c["value"] / a["value"] < 1.3, (a["value"], c["value"])

@@ -1,0 +1,519 @@
+// sched_probe.hip -- work-distribution probes on the GPU box (not product
+// code).  A pure nontemporal read stream with the CRC kernel's access shape
+// (8-lane groups walking 128-byte rows, 8 rows in flight per lane, one
+// 1024-thread workgroup per CU, 16 waves), over 1 GiB, with three schedules:
+//   static   every wave reads an equal contiguous share (the r01 schedule)
+//   claims   the same shares, but each wave claims its next S rows with a
+//            64-bit atomicAdd on its own control word one step ahead
+//            (measures what the claims cost while the chip streams)
+//   steal    claims + work stealing: a wave whose share is exhausted samples
+//            64 other waves' control words in one vector load, takes half of
+//            the largest remainder from its end with a 64-bit CAS, and
+//            continues (its own word then holds the stolen range, so it can
+//            be stolen from in turn)
+//   xcd      static shares per XCD in proportion to weights the host
+//            recalibrates from the previous launches' per-XCD finish times
+//            (each workgroup takes a slot on its XCD with one atomicAdd at
+//            entry; s_memrealtime telemetry per workgroup)
+// and a read+write copy probe (same shape, nontemporal loads and stores):
+// the denominator for the fused CRC + copy kernel.
+// Build: make build/sched_probe.  Output: one JSON object.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4w;
+
+#define CHECK(x)                                                               \
+	do {                                                                   \
+		hipError_t e = (x);                                            \
+		if (e != hipSuccess) {                                         \
+			fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); \
+			exit(1);                                               \
+		}                                                              \
+	} while (0)
+
+#define D 8          // rows in flight per lane
+#define WAVES 16     // per workgroup
+#define ROW 128u
+
+__device__ __forceinline__ uint32_t uni(uint32_t v)
+{
+	return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ u32x4 ld(const uint8_t *p, uint64_t row, uint32_t g8)
+{
+	return __builtin_nontemporal_load((g_u32x4 *)(p + row * ROW + 16u * g8));
+}
+
+__device__ __forceinline__ uint64_t ctl_pack(uint32_t b, uint32_t e)
+{
+	return ((uint64_t)e << 32) | b;
+}
+
+// One step = rows [b, b + n) of the row space, the 8 groups taking 8
+// contiguous slices.  Per lane: first row and count.
+struct PStep {
+	uint32_t row, n; // this lane's group slice
+	uint32_t T;      // max slice length (loop trip count), 0 = no step
+};
+
+__device__ __forceinline__ PStep make_step(uint32_t b, uint32_t n, uint32_t grp)
+{
+	PStep s;
+	const uint32_t q = n >> 3, rm = n & 7u;
+	s.row = b + grp * q + min(grp, rm);
+	s.n = q + (grp < rm ? 1u : 0u);
+	s.T = n ? q + (rm ? 1u : 0u) : 0u;
+	return s;
+}
+
+// steal: returns the first step of the stolen range (T == 0: nothing found)
+template <bool STEAL>
+__device__ __forceinline__ PStep steal(uint64_t *ctl, uint32_t W, uint32_t w, uint32_t S, uint32_t lane, uint32_t grp,
+				       uint32_t *nsteal)
+{
+	PStep none;
+	none.T = 0;
+	none.row = none.n = 0;
+	if (!STEAL)
+		return none;
+	for (uint32_t attempt = 0; attempt < 4; ++attempt) {
+		const uint32_t cand = (w + 1u + (lane + 64u * attempt) * 67u) % W;
+		const uint64_t v = __hip_atomic_load(ctl + cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		const uint32_t b = (uint32_t)v, e = (uint32_t)(v >> 32);
+		uint32_t rem = e > b ? e - b : 0u;
+		// wave max of rem, and the lowest lane holding it
+		uint32_t m = rem;
+#pragma unroll
+		for (uint32_t d = 1; d < 64; d <<= 1)
+			m = max(m, (uint32_t)__shfl_xor(m, d));
+		m = uni(m);
+		if (m < 2u * S)
+			continue;
+		const uint64_t hit = __ballot(rem == m);
+		const uint32_t src = (uint32_t)__builtin_ctzll(hit);
+		const uint32_t vc = uni(__shfl(cand, src));
+		uint64_t cur = __shfl(v, src);
+		for (uint32_t tries = 0; tries < 3; ++tries) {
+			const uint32_t cb = uni((uint32_t)cur), ce = uni((uint32_t)(cur >> 32));
+			if (ce <= cb || ce - cb < 2u * S)
+				break;
+			const uint32_t K = ((ce - cb) / 2u) / S * S;
+			uint64_t prev = 0;
+			if (lane == 0) {
+				uint64_t expct = cur;
+				__hip_atomic_compare_exchange_strong(ctl + vc, &expct, ctl_pack(cb, ce - K), __ATOMIC_RELAXED,
+								     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				prev = expct; // the value seen (== cur on success)
+			}
+			prev = ((uint64_t)uni((uint32_t)(__shfl(prev, 0) >> 32)) << 32) | uni((uint32_t)__shfl(prev, 0));
+			if (prev == cur) {
+				// [ce - K, ce) is ours; the first S rows are taken now
+				const uint32_t s0 = ce - K;
+				if (lane == 0) {
+					__hip_atomic_exchange(ctl + w, ctl_pack(s0 + S, ce), __ATOMIC_RELAXED,
+							      __HIP_MEMORY_SCOPE_AGENT);
+					atomicAdd(nsteal, 1u);
+				}
+				return make_step(s0, S, grp);
+			}
+			cur = prev;
+		}
+	}
+	return none;
+}
+
+template <int MODE> // 0 static, 1 claims, 2 steal
+__global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R, uint64_t *ctl, uint32_t S,
+						    uint32_t *out, uint32_t *nsteal)
+{
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	u32x4 acc = (u32x4)(0u), ring[D];
+	PStep cur;
+	if (MODE == 0) {
+		cur = make_step(r0, r1 - r0, grp); // the whole share is one step
+	} else {
+		const uint32_t n0 = min(S, r1 - r0);
+		if (lane == 0)
+			__hip_atomic_exchange(ctl + w, ctl_pack(r0 + n0, r1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		cur = make_step(r0, n0, grp);
+	}
+	if (cur.T == 0)
+		return;
+#pragma unroll
+	for (int i = 0; i + 1 < D; ++i)
+		ring[i] = ld(p, cur.row + min((uint32_t)i, cur.n - 1u), g8);
+	while (cur.T) {
+		// claim the step after this one now: consumed at this step's end
+		uint64_t fut = 0;
+		if (MODE != 0 && lane == 0)
+			fut = __hip_atomic_fetch_add(ctl + w, (uint64_t)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		const uint32_t nblk = (cur.T + D - 1) / D;
+		uint32_t blk = 0;
+		for (; blk + 1 < nblk; ++blk) {
+#pragma unroll
+			for (int i = 0; i < D; ++i) {
+				const uint32_t r = blk * D + i;
+				ring[(i + D - 1) % D] = ld(p, cur.row + min(r + D - 1, cur.n - 1u), g8);
+				acc ^= ring[i];
+			}
+		}
+		// next step
+		PStep nxt;
+		nxt.T = 0;
+		nxt.row = nxt.n = 0;
+		if (MODE != 0) {
+			fut = __shfl(fut, 0);
+			const uint32_t b = uni((uint32_t)fut), e = uni((uint32_t)(fut >> 32));
+			if (b < e)
+				nxt = make_step(b, min(S, e - b), grp);
+			else
+				nxt = steal<MODE == 2>(ctl, W, w, S, lane, grp, nsteal);
+		}
+		const bool more = nxt.T != 0;
+		const uint32_t r = blk * D;
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			const uint32_t ri = r + i;
+			// the last block's prefetch already fetches the next step's first rows
+			const uint32_t lr = ri + D - 1;
+			if (i == 0)
+				ring[D - 1] = ld(p, cur.row + min(lr, cur.n - 1u), g8);
+			else
+				ring[i - 1] = more ? ld(p, nxt.row + min((uint32_t)(i - 1), nxt.n - 1u), g8)
+						   : ld(p, cur.row + cur.n - 1u, g8);
+			if (ri < cur.n)
+				acc ^= ring[i];
+		}
+		cur = nxt;
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[w] = x;
+}
+
+// XCD-weighted static: XCD x streams rows [X[x], X[x+1]) split over the
+// workgroups that land on it (slot from a per-XCD counter), 16 waves each
+__global__ __launch_bounds__(1024, 1) void k_xcd(const uint8_t *p, uint32_t R, const uint32_t *X, uint32_t *slots,
+						 uint32_t nslot, uint64_t *tele, uint32_t *out)
+{
+	__shared__ uint32_t s_slot, s_xcc;
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t wv = threadIdx.x / 64u;
+	const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+	if (threadIdx.x == 0) {
+		uint32_t xcc;
+		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+		s_xcc = xcc & 7u;
+		s_slot = atomicAdd(slots + (xcc & 7u), 1u);
+	}
+	__syncthreads();
+	const uint32_t xcc = s_xcc, slot = s_slot;
+	u32x4 acc = (u32x4)(0u), ring[D];
+	if (slot < nslot) {
+		const uint32_t a = X[xcc], b = X[xcc + 1];
+		const uint32_t ws0 = a + (uint32_t)((uint64_t)(b - a) * slot / nslot);
+		const uint32_t ws1 = a + (uint32_t)((uint64_t)(b - a) * (slot + 1) / nslot);
+		const uint32_t r0 = ws0 + (uint32_t)((uint64_t)(ws1 - ws0) * wv / WAVES);
+		const uint32_t r1 = ws0 + (uint32_t)((uint64_t)(ws1 - ws0) * (wv + 1) / WAVES);
+		const PStep s = make_step(r0, r1 - r0, grp);
+		if (s.T) {
+#pragma unroll
+			for (int i = 0; i + 1 < D; ++i)
+				ring[i] = ld(p, s.row + min((uint32_t)i, s.n - 1u), g8);
+			for (uint32_t r = 0; r < s.T; r += D) {
+#pragma unroll
+				for (int i = 0; i < D; ++i) {
+					ring[(i + D - 1) % D] = ld(p, s.row + min(r + i + D - 1, s.n - 1u), g8);
+					if (r + i < s.n)
+						acc ^= ring[i];
+				}
+			}
+		}
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[blockIdx.x] = x;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		tele[3 * blockIdx.x] = t0;
+		tele[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+		tele[3 * blockIdx.x + 2] = ((uint64_t)slot << 8) | xcc;
+	}
+}
+
+// Global pool: units of S rows, handed out by NC counters (counter k serves
+// units k, k + NC, ...; wave w draws from counter w % NC, so every counter
+// sees waves of every XCD).  Each wave keeps AHEAD claims in flight: the
+// claim for step i + AHEAD is issued when step i starts, so an atomic's
+// latency under streaming load (~10-20 us) is covered by AHEAD steps.
+template <int AHEAD>
+__global__ __launch_bounds__(1024, 1) void k_pool(const uint8_t *p, uint32_t R, uint32_t *ctr, uint32_t S, uint32_t NC,
+						  uint32_t *out)
+{
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t k = w % NC;
+	const uint32_t nunits = (R + S - 1) / S;
+	uint32_t q[AHEAD + 1]; // claimed unit indices, oldest first (lane 0's results)
+#pragma unroll
+	for (int i = 0; i <= AHEAD; ++i)
+		q[i] = lane == 0 ? atomicAdd(ctr + k, 1u) : 0u;
+	auto unit_step = [&](uint32_t c) {
+		const uint32_t u = k + NC * uni(__shfl(c, 0));
+		PStep s;
+		if (u >= nunits) {
+			s.T = 0;
+			s.row = s.n = 0;
+			return s;
+		}
+		return make_step(u * S, min(S, R - u * S), grp);
+	};
+	PStep cur = unit_step(q[0]);
+	u32x4 acc = (u32x4)(0u), ring[D];
+	if (cur.T == 0)
+		return;
+#pragma unroll
+	for (int i = 0; i + 1 < D; ++i)
+		ring[i] = ld(p, cur.row + min((uint32_t)i, cur.n - 1u), g8);
+	while (cur.T) {
+		// shift the claim queue, claim one more
+#pragma unroll
+		for (int i = 0; i < AHEAD; ++i)
+			q[i] = q[i + 1];
+		q[AHEAD] = lane == 0 ? atomicAdd(ctr + k, 1u) : 0u;
+		const uint32_t nblk = (cur.T + D - 1) / D;
+		uint32_t blk = 0;
+		for (; blk + 1 < nblk; ++blk) {
+#pragma unroll
+			for (int i = 0; i < D; ++i) {
+				const uint32_t r = blk * D + i;
+				ring[(i + D - 1) % D] = ld(p, cur.row + min(r + D - 1, cur.n - 1u), g8);
+				acc ^= ring[i];
+			}
+		}
+		const PStep nxt = unit_step(q[0]);
+		const bool more = nxt.T != 0;
+		const uint32_t r = blk * D;
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			const uint32_t ri = r + i;
+			if (i == 0)
+				ring[D - 1] = ld(p, cur.row + min(ri + D - 1, cur.n - 1u), g8);
+			else
+				ring[i - 1] = more ? ld(p, nxt.row + min((uint32_t)(i - 1), nxt.n - 1u), g8)
+						   : ld(p, cur.row + cur.n - 1u, g8);
+			if (ri < cur.n)
+				acc ^= ring[i];
+		}
+		cur = nxt;
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[w] = x;
+}
+
+// read+write copy, static shares, same shape
+__global__ __launch_bounds__(1024, 1) void k_copy(const uint8_t *p, uint8_t *q, uint32_t R)
+{
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const PStep s = make_step(r0, r1 - r0, grp);
+	u32x4 ring[D];
+	for (uint32_t r = 0; r < s.n; r += D) {
+#pragma unroll
+		for (int i = 0; i < D; ++i)
+			ring[i] = ld(p, s.row + min(r + i, s.n - 1u), g8);
+#pragma unroll
+		for (int i = 0; i < D; ++i)
+			if (r + i < s.n)
+				__builtin_nontemporal_store(ring[i], (g_u32x4w *)(q + (uint64_t)(s.row + r + i) * ROW + 16u * g8));
+	}
+}
+
+int main(int argc, char **argv)
+{
+	const size_t bytes = (size_t)1 << 30;
+	const uint32_t R = (uint32_t)(bytes / ROW);
+	hipDeviceProp_t prop;
+	CHECK(hipGetDeviceProperties(&prop, 0));
+	const int ncu = prop.multiProcessorCount;
+	const uint32_t W = ncu * WAVES;
+	uint8_t *buf[3];
+	for (int i = 0; i < 3; ++i) {
+		CHECK(hipMalloc(&buf[i], bytes));
+		CHECK(hipMemset(buf[i], i + 1, bytes));
+	}
+	uint64_t *ctl;
+	uint32_t *out, *nsteal;
+	CHECK(hipMalloc(&ctl, W * 8u));
+	CHECK(hipMalloc(&out, W * 4u));
+	CHECK(hipMalloc(&nsteal, 4u));
+	const int reps = argc > 1 ? atoi(argv[1]) : 20;
+	hipEvent_t e0, e1;
+	CHECK(hipEventCreate(&e0));
+	CHECK(hipEventCreate(&e1));
+	struct {
+		const char *name;
+		int mode;
+		uint32_t S;
+	} runs[] = {{"static", 0, 0},     {"claims S256", 1, 256}, {"steal S256", 2, 256}, {"steal S128", 2, 128},
+		    {"steal S64", 2, 64}, {"claims S128", 1, 128}, {"static (again)", 0, 0}};
+	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, ncu, bytes);
+	for (size_t k = 0; k < sizeof(runs) / sizeof(runs[0]); ++k) {
+		float tot = 0, best = 1e9f;
+		uint32_t steals = 0;
+		for (int r = -2; r < reps; ++r) {
+			CHECK(hipMemsetAsync(ctl, 0, W * 8u, 0));
+			CHECK(hipMemsetAsync(nsteal, 0, 4u, 0));
+			CHECK(hipEventRecord(e0, 0));
+			const uint8_t *p = buf[(r + 4) % 2];
+			if (runs[k].mode == 0)
+				hipLaunchKernelGGL(k_sched<0>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
+			else if (runs[k].mode == 1)
+				hipLaunchKernelGGL(k_sched<1>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
+			else
+				hipLaunchKernelGGL(k_sched<2>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
+			CHECK(hipEventRecord(e1, 0));
+			CHECK(hipEventSynchronize(e1));
+			float ms;
+			CHECK(hipEventElapsedTime(&ms, e0, e1));
+			if (r >= 0) {
+				tot += ms;
+				best = ms < best ? ms : best;
+			}
+			CHECK(hipMemcpy(&steals, nsteal, 4, hipMemcpyDeviceToHost));
+		}
+		printf("  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f, \"steals_last\": %u},\n",
+		       runs[k].name, tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9, steals);
+	}
+	{
+		// global pool with claims AHEAD steps ahead
+		uint32_t *ctr;
+		CHECK(hipMalloc(&ctr, 64 * 4));
+		struct {
+			const char *name;
+			int ahead;
+			uint32_t S, NC;
+		} pr[] = {{"pool S256 ahead1 nc8", 1, 256, 8},  {"pool S256 ahead2 nc8", 2, 256, 8},
+			  {"pool S128 ahead2 nc8", 2, 128, 8},  {"pool S128 ahead3 nc8", 3, 128, 8},
+			  {"pool S64 ahead3 nc16", 3, 64, 16},  {"pool S256 ahead2 nc32", 2, 256, 32},
+			  {"pool S128 ahead3 nc32", 3, 128, 32}};
+		for (size_t k = 0; k < sizeof(pr) / sizeof(pr[0]); ++k) {
+			float tot = 0, best = 1e9f;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipMemsetAsync(ctr, 0, 64 * 4, 0));
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *p = buf[(r + 4) % 2];
+				if (pr[k].ahead == 1)
+					hipLaunchKernelGGL(k_pool<1>, dim3(ncu), dim3(1024), 0, 0, p, R, ctr, pr[k].S, pr[k].NC, out);
+				else if (pr[k].ahead == 2)
+					hipLaunchKernelGGL(k_pool<2>, dim3(ncu), dim3(1024), 0, 0, p, R, ctr, pr[k].S, pr[k].NC, out);
+				else
+					hipLaunchKernelGGL(k_pool<3>, dim3(ncu), dim3(1024), 0, 0, p, R, ctr, pr[k].S, pr[k].NC, out);
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0) {
+					tot += ms;
+					best = ms < best ? ms : best;
+				}
+			}
+			printf("  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f},\n", pr[k].name,
+			       tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	{
+		// XCD-weighted static, weights recalibrated after every launch
+		uint32_t *X, *slots;
+		uint64_t *tele;
+		CHECK(hipMalloc(&X, 9 * 4));
+		CHECK(hipMalloc(&slots, 8 * 4));
+		CHECK(hipMalloc(&tele, (size_t)ncu * 3 * 8));
+		std::vector<uint64_t> ht((size_t)ncu * 3);
+		double w[8];
+		for (int x = 0; x < 8; ++x)
+			w[x] = 1.0 / 8;
+		const uint32_t nslot = (ncu + 7) / 8;
+		const int cal = 20;
+		float tot = 0, first = 0;
+		char hist[4096];
+		int hl = 0;
+		for (int r = 0; r < cal + reps; ++r) {
+			uint32_t hx[9];
+			double acc = 0;
+			hx[0] = 0;
+			for (int x = 0; x < 8; ++x) {
+				acc += w[x];
+				hx[x + 1] = x == 7 ? R : (uint32_t)(acc * R);
+			}
+			CHECK(hipMemcpy(X, hx, 9 * 4, hipMemcpyHostToDevice));
+			CHECK(hipMemset(slots, 0, 8 * 4));
+			CHECK(hipEventRecord(e0, 0));
+			hipLaunchKernelGGL(k_xcd, dim3(ncu), dim3(1024), 0, 0, buf[r % 2], R, X, slots, nslot, tele, out);
+			CHECK(hipEventRecord(e1, 0));
+			CHECK(hipEventSynchronize(e1));
+			float ms;
+			CHECK(hipEventElapsedTime(&ms, e0, e1));
+			if (r == 0)
+				first = ms;
+			if (r >= cal)
+				tot += ms;
+			CHECK(hipMemcpy(ht.data(), tele, ht.size() * 8, hipMemcpyDeviceToHost));
+			uint64_t tmin = ~0ull, tend[8] = {0};
+			for (int b = 0; b < ncu; ++b) {
+				tmin = ht[3 * b] < tmin ? ht[3 * b] : tmin;
+				const int x = (int)(ht[3 * b + 2] & 7u);
+				tend[x] = ht[3 * b + 1] > tend[x] ? ht[3 * b + 1] : tend[x];
+			}
+			double rate[8], rs = 0;
+			for (int x = 0; x < 8; ++x) {
+				rate[x] = w[x] / (double)(tend[x] - tmin);
+				rs += rate[x];
+			}
+			for (int x = 0; x < 8; ++x)
+				w[x] = 0.5 * w[x] + 0.5 * rate[x] / rs;
+			if (r < 6 || r == cal + reps - 1) {
+				hl += snprintf(hist + hl, sizeof(hist) - hl, "%s[%.1f", hl ? ", " : "", ms * 1e3);
+				for (int x = 0; x < 8; ++x)
+					hl += snprintf(hist + hl, sizeof(hist) - hl, ", %.1f", (tend[x] - tmin) / 100.0);
+				hl += snprintf(hist + hl, sizeof(hist) - hl, "]");
+			}
+		}
+		printf("  {\"probe\": \"xcd-weighted static\", \"us\": %.2f, \"first_us\": %.2f, \"GBps\": %.1f, "
+		       "\"weights\": [%.4f, %.4f, %.4f, %.4f, %.4f, %.4f, %.4f, %.4f], "
+		       "\"launch_us_and_xcd_end_us\": [%s]},\n",
+		       tot / reps * 1e3, first * 1e3, bytes / (tot / reps * 1e-3) / 1e9, w[0], w[1], w[2], w[3], w[4], w[5],
+		       w[6], w[7], hist);
+	}
+	{
+		float tot = 0;
+		for (int r = -2; r < reps; ++r) {
+			CHECK(hipEventRecord(e0, 0));
+			hipLaunchKernelGGL(k_copy, dim3(ncu), dim3(1024), 0, 0, buf[(r + 4) % 2], buf[2], R);
+			CHECK(hipEventRecord(e1, 0));
+			CHECK(hipEventSynchronize(e1));
+			float ms;
+			CHECK(hipEventElapsedTime(&ms, e0, e1));
+			if (r >= 0)
+				tot += ms;
+		}
+		printf("  {\"probe\": \"copy static (read+write)\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}\n",
+		       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+	}
+	printf("]}\n");
+	return 0;
+}
