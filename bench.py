@@ -294,6 +294,10 @@ def main():
 
     if len(shards) > 1:
         line["shards_checked"] = shard_parity(shards, offs, sizes, rotate, P)
+    if rank == 0 and world == 1 and len(shards) == 1 and launches:
+        probe = stream_probe("copy" if dsts else "read")
+        if probe:
+            line["roofline"]["probe"] = dict(probe, frac_of_probe=round(achieved_gbs / probe["GBps"], 4))
 
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -443,6 +447,25 @@ def msgr_c_bench(args, size, count):
             "path": f"C: crc32c_async_submit per {size}-byte payload from crc32c_pages memory, flush every 64, "
                     "drain via eventfd (build/msgr_sim bench); zerocopy: kernel reads pinned payloads below 1 MiB in place, larger ones DMA'd",
             "payloads": count, "passes": args.host_passes, "matches_oracle": True}
+
+
+def stream_probe(kind):
+    """The same box's streaming ceiling for the kernel's access shape
+    (build/sched_probe, tools/sched_probe.hip: 1 GiB, 8-lane groups over
+    128-byte rows, 8 rows in flight per lane, nontemporal, one 1024-thread
+    workgroup per CU, equal static shares): "read" for the CRC kernel, "copy"
+    (read + write) for the fused CRC + copy.  None if the probe is missing."""
+    exe = os.path.join(REPO, "build", "sched_probe")
+    if not os.path.exists(exe):
+        return None
+    r = subprocess.run([exe, "10", kind], capture_output=True, timeout=120)
+    if r.returncode != 0:
+        return None
+    res = json.loads(r.stdout.decode())["results"][0]
+    gbs = res.get("GBps_read_plus_write", res.get("GBps"))
+    return {"kind": kind, "GBps": gbs, "us_per_GiB": res["us"],
+            "what": "tools/sched_probe.hip: same access shape, nontemporal, static shares, 1 GiB" +
+                    (" read + 1 GiB written" if kind == "copy" else " read")}
 
 
 def shard_parity(shards, offs, sizes, rotate, P):

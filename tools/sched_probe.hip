@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <vector>
 
@@ -343,8 +344,17 @@ __global__ __launch_bounds__(1024, 1) void k_copy(const uint8_t *p, uint8_t *q, 
 	}
 }
 
+static int g_entries;
+static const char *sep(void)
+{
+	return g_entries++ ? ",\n" : "";
+}
+
+// usage: sched_probe [reps] [all|read|copy]   (read: the static read stream only)
 int main(int argc, char **argv)
 {
+	const char *which = argc > 2 ? argv[2] : "all";
+	const bool all = !strcmp(which, "all"), only_read = !strcmp(which, "read"), only_copy = !strcmp(which, "copy");
 	const size_t bytes = (size_t)1 << 30;
 	const uint32_t R = (uint32_t)(bytes / ROW);
 	hipDeviceProp_t prop;
@@ -373,6 +383,8 @@ int main(int argc, char **argv)
 		    {"steal S64", 2, 64}, {"claims S128", 1, 128}, {"static (again)", 0, 0}};
 	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, ncu, bytes);
 	for (size_t k = 0; k < sizeof(runs) / sizeof(runs[0]); ++k) {
+		if (only_copy || (only_read && runs[k].mode != 0))
+			continue;
 		float tot = 0, best = 1e9f;
 		uint32_t steals = 0;
 		for (int r = -2; r < reps; ++r) {
@@ -396,10 +408,10 @@ int main(int argc, char **argv)
 			}
 			CHECK(hipMemcpy(&steals, nsteal, 4, hipMemcpyDeviceToHost));
 		}
-		printf("  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f, \"steals_last\": %u},\n",
-		       runs[k].name, tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9, steals);
+		printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f, \"steals_last\": %u}",
+		       sep(), runs[k].name, tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9, steals);
 	}
-	{
+	if (all) {
 		// global pool with claims AHEAD steps ahead
 		uint32_t *ctr;
 		CHECK(hipMalloc(&ctr, 64 * 4));
@@ -432,11 +444,11 @@ int main(int argc, char **argv)
 					best = ms < best ? ms : best;
 				}
 			}
-			printf("  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f},\n", pr[k].name,
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f}", sep(), pr[k].name,
 			       tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9);
 		}
 	}
-	{
+	if (all) {
 		// XCD-weighted static, weights recalibrated after every launch
 		uint32_t *X, *slots;
 		uint64_t *tele;
@@ -493,13 +505,13 @@ int main(int argc, char **argv)
 				hl += snprintf(hist + hl, sizeof(hist) - hl, "]");
 			}
 		}
-		printf("  {\"probe\": \"xcd-weighted static\", \"us\": %.2f, \"first_us\": %.2f, \"GBps\": %.1f, "
+		printf("%s  {\"probe\": \"xcd-weighted static\", \"us\": %.2f, \"first_us\": %.2f, \"GBps\": %.1f, "
 		       "\"weights\": [%.4f, %.4f, %.4f, %.4f, %.4f, %.4f, %.4f, %.4f], "
-		       "\"launch_us_and_xcd_end_us\": [%s]},\n",
-		       tot / reps * 1e3, first * 1e3, bytes / (tot / reps * 1e-3) / 1e9, w[0], w[1], w[2], w[3], w[4], w[5],
+		       "\"launch_us_and_xcd_end_us\": [%s]}",
+		       sep(), tot / reps * 1e3, first * 1e3, bytes / (tot / reps * 1e-3) / 1e9, w[0], w[1], w[2], w[3], w[4], w[5],
 		       w[6], w[7], hist);
 	}
-	{
+	if (all || only_copy) {
 		float tot = 0;
 		for (int r = -2; r < reps; ++r) {
 			CHECK(hipEventRecord(e0, 0));
@@ -511,9 +523,9 @@ int main(int argc, char **argv)
 			if (r >= 0)
 				tot += ms;
 		}
-		printf("  {\"probe\": \"copy static (read+write)\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}\n",
-		       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		printf("%s  {\"probe\": \"copy static (read+write)\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}",
+		       sep(), tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
 	}
-	printf("]}\n");
+	printf("\n]}\n");
 	return 0;
 }
