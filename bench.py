@@ -84,6 +84,10 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
     ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
+    ap.add_argument("--sustain-seconds", type=float, default=6.0,
+                    help="after the K timed steps, keep the value pass running this long and report its rate as "
+                         "`sustained` (seconds of GPU work: clocks/thermals settle, a sampling monitor sees the GPU "
+                         "busy); 0 = skip")
     ap.add_argument("--single-thread", action="store_true",
                     help="pech's model: ONE process drives --gpus devices (hipSetDevice + crc32c_dev_batch_ws_async "
                          "per device, own streams and workspaces), instead of one process per GPU")
@@ -227,6 +231,9 @@ def main():
     elapsed = serial_el if nstreams == 1 else timed(nstreams, args.steps, args.warmup)[0]
     launches = len(samples)
     kernel_ms = float(samples.sum()) / 1e3
+    sustained = None
+    if args.sustain_seconds > 0:
+        sustained = sustain(shards, nstreams, args.sustain_seconds, sync_all, dist, backend, dev, torch)
 
     total_bytes = batch_bytes * args.steps * world * len(shards)
     value = total_bytes / elapsed / (1 << 30)
@@ -292,6 +299,11 @@ def main():
     if rank == 0 and world == 1 and len(shards) == 1 and not args.no_cpu_baseline and not dsts:
         line["cpu_baseline"] = cpu_baseline(args, bufs[0], offs, sizes, outs, rotate, P)
 
+    if sustained:
+        sec, steps_done = sustained
+        line["sustained"] = {"seconds": round(sec, 2), "steps": steps_done, "streams": nstreams,
+                             "value": round(batch_bytes * steps_done * world * len(shards) / sec / (1 << 30), 2),
+                             "unit": "GiB/s"}
     if len(shards) > 1:
         line["shards_checked"] = shard_parity(shards, offs, sizes, rotate, P)
     if rank == 0 and world == 1 and len(shards) == 1 and launches:
@@ -447,6 +459,36 @@ def msgr_c_bench(args, size, count):
             "path": f"C: crc32c_async_submit per {size}-byte payload from crc32c_pages memory, flush every 64, "
                     "drain via eventfd (build/msgr_sim bench); zerocopy: kernel reads pinned payloads below 1 MiB in place, larger ones DMA'd",
             "payloads": count, "passes": args.host_passes, "matches_oracle": True}
+
+
+def sustain(shards, nstreams, seconds, sync_all, dist, backend, dev, torch):
+    """The value pass kept running for `seconds` (batch i on stream i % nstreams
+    of every shard), in rounds of 64 steps; returns (elapsed, steps), elapsed
+    max over ranks and every rank running the same number of rounds."""
+    sync_all()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        for i in range(64):
+            for sh in shards:
+                sh.step(steps + i, (steps + i) % nstreams)
+        steps += 64
+        sync_all()
+        go = time.perf_counter() - t0 < seconds
+        if dist is not None:  # all ranks stop after the same round
+            t = torch.tensor([1 if go else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            go = bool(t.item())
+        if not go:
+            break
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, steps
 
 
 def stream_probe(kind):

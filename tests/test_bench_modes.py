@@ -12,7 +12,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-COMMON = ["--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--no-host-path"]
+COMMON = ["--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--no-host-path", "--sustain-seconds", "0.5"]
 
 
 def run(*extra):

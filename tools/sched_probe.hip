@@ -350,12 +350,13 @@ static const char *sep(void)
 	return g_entries++ ? ",\n" : "";
 }
 
-// usage: sched_probe [reps] [all|read|copy]   (read: the static read stream only)
+// usage: sched_probe [reps] [all|read|copy] [MiB per launch, default 1024]
+// (read: the static read stream only)
 int main(int argc, char **argv)
 {
 	const char *which = argc > 2 ? argv[2] : "all";
 	const bool all = !strcmp(which, "all"), only_read = !strcmp(which, "read"), only_copy = !strcmp(which, "copy");
-	const size_t bytes = (size_t)1 << 30;
+	const size_t bytes = (size_t)(argc > 3 ? atoi(argv[3]) : 1024) << 20;
 	const uint32_t R = (uint32_t)(bytes / ROW);
 	hipDeviceProp_t prop;
 	CHECK(hipGetDeviceProperties(&prop, 0));
