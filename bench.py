@@ -84,10 +84,12 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
     ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
+    ap.add_argument("--rotate", type=int, default=None,
+                    help="distinct resident batches to rotate over (default per config; a multiple of --streams)")
     ap.add_argument("--sustain-seconds", type=float, default=6.0,
-                    help="after the K timed steps, keep the value pass running this long and report its rate as "
-                         "`sustained` (seconds of GPU work: clocks/thermals settle, a sampling monitor sees the GPU "
-                         "busy); 0 = skip")
+                    help="before the warm-up and the K timed steps, run the value pass this long and report its "
+                         "rate as `sustained` (seconds of GPU work: clocks/thermals settle before the timed steps, a "
+                         "sampling monitor sees the GPU busy); 0 = skip")
     ap.add_argument("--single-thread", action="store_true",
                     help="pech's model: ONE process drives --gpus devices (hipSetDevice + crc32c_dev_batch_ws_async "
                          "per device, own streams and workspaces), instead of one process per GPU")
@@ -132,6 +134,9 @@ def main():
     from pech_amd import _lib
 
     sizes, rotate, desc = CONFIGS[args.config]
+    if args.rotate:
+        rotate = args.rotate
+        desc = desc.split(",")[0] + f", {rotate} rotating batches"
     if sizes is None:
         sizes = c4_sizes()
     sizes = np.asarray(sizes, dtype=np.int64)
@@ -227,13 +232,16 @@ def main():
     # tail overlap its neighbour's streaming -- how a server runs the library
     # (the async layer keeps four batches in flight).  Pass 2 is `value`.
     nstreams = max(1, args.streams)
+    # The sustained pass runs first: seconds of the value pass, so clocks and
+    # thermals have settled before the K timed steps (a 20-step pass lasts
+    # ~4 ms), and a sampling GPU monitor sees the device busy.
+    sustained = None
+    if args.sustain_seconds > 0:
+        sustained = sustain(shards, nstreams, args.sustain_seconds, sync_all, dist, backend, dev, torch)
     serial_el, samples = timed(1, args.steps, args.warmup)
     elapsed = serial_el if nstreams == 1 else timed(nstreams, args.steps, args.warmup)[0]
     launches = len(samples)
     kernel_ms = float(samples.sum()) / 1e3
-    sustained = None
-    if args.sustain_seconds > 0:
-        sustained = sustain(shards, nstreams, args.sustain_seconds, sync_all, dist, backend, dev, torch)
 
     total_bytes = batch_bytes * args.steps * world * len(shards)
     value = total_bytes / elapsed / (1 << 30)
