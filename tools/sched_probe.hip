@@ -324,6 +324,75 @@ __global__ __launch_bounds__(1024, 1) void k_pool(const uint8_t *p, uint32_t R, 
 		out[w] = x;
 }
 
+// Workgroup pool: the workgroup's contiguous range (an equal 1/grid share of
+// the rows) is cut into items of S rows; its 16 waves take items in order
+// with an LDS counter (ds_add_rtn, no device atomics), each wave claiming its
+// next item AHEAD one item early.  Waves of one CU then finish within about
+// one item of each other, whatever their issue priority.
+__global__ __launch_bounds__(1024, 1) void k_wgpool(const uint8_t *p, uint32_t R, uint32_t S, uint32_t *out)
+{
+	__shared__ uint32_t next_item;
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t b0 = (uint32_t)((uint64_t)R * blockIdx.x / gridDim.x);
+	const uint32_t b1 = (uint32_t)((uint64_t)R * (blockIdx.x + 1) / gridDim.x);
+	const uint32_t nitems = (b1 - b0 + S - 1) / S;
+	if (threadIdx.x == 0)
+		next_item = WAVES; // items 0..15 go to waves 0..15 without a claim
+	__syncthreads();
+	const uint32_t wv = threadIdx.x / 64u;
+	auto item_step = [&](uint32_t it) {
+		PStep s;
+		if (it >= nitems) {
+			s.T = 0;
+			s.row = s.n = 0;
+			return s;
+		}
+		const uint32_t a = b0 + it * S;
+		return make_step(a, min(S, b1 - a), grp);
+	};
+	PStep cur = item_step(wv);
+	u32x4 acc = (u32x4)(0u), ring[D];
+	if (cur.T) {
+#pragma unroll
+		for (int i = 0; i + 1 < D; ++i)
+			ring[i] = ld(p, cur.row + min((uint32_t)i, cur.n - 1u), g8);
+	}
+	while (cur.T) {
+		uint32_t claim = 0;
+		if (lane == 0)
+			claim = atomicAdd(&next_item, 1u);
+		const uint32_t nblk = (cur.T + D - 1) / D;
+		uint32_t blk = 0;
+		for (; blk + 1 < nblk; ++blk) {
+#pragma unroll
+			for (int i = 0; i < D; ++i) {
+				const uint32_t r = blk * D + i;
+				ring[(i + D - 1) % D] = ld(p, cur.row + min(r + D - 1, cur.n - 1u), g8);
+				acc ^= ring[i];
+			}
+		}
+		const PStep nxt = item_step(uni(__shfl(claim, 0)));
+		const bool more = nxt.T != 0;
+		const uint32_t r = blk * D;
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			const uint32_t ri = r + i;
+			if (i == 0)
+				ring[D - 1] = ld(p, cur.row + min(ri + D - 1, cur.n - 1u), g8);
+			else
+				ring[i - 1] = more ? ld(p, nxt.row + min((uint32_t)(i - 1), nxt.n - 1u), g8)
+						   : ld(p, cur.row + cur.n - 1u, g8);
+			if (ri < cur.n)
+				acc ^= ring[i];
+		}
+		cur = nxt;
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[w] = x;
+}
+
 // read+write copy, static shares, same shape
 __global__ __launch_bounds__(1024, 1) void k_copy(const uint8_t *p, uint8_t *q, uint32_t R)
 {
@@ -384,7 +453,7 @@ int main(int argc, char **argv)
 		    {"steal S64", 2, 64}, {"claims S128", 1, 128}, {"static (again)", 0, 0}};
 	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, ncu, bytes);
 	for (size_t k = 0; k < sizeof(runs) / sizeof(runs[0]); ++k) {
-		if (only_copy || (only_read && runs[k].mode != 0))
+		if (only_copy || (!all && runs[k].mode != 0) || (!all && !only_read))
 			continue;
 		float tot = 0, best = 1e9f;
 		uint32_t steals = 0;
@@ -411,6 +480,28 @@ int main(int argc, char **argv)
 		}
 		printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f, \"steals_last\": %u}",
 		       sep(), runs[k].name, tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9, steals);
+	}
+	if (all || !strcmp(which, "wgpool")) {
+		// workgroup pools: items of S rows claimed through LDS
+		const uint32_t Ss[] = {512, 256, 128, 64};
+		for (int pass = 0; pass < 2; ++pass)
+			for (uint32_t S : Ss) {
+				float tot = 0, best = 1e9f;
+				for (int r = -2; r < reps; ++r) {
+					CHECK(hipEventRecord(e0, 0));
+					hipLaunchKernelGGL(k_wgpool, dim3(ncu), dim3(1024), 0, 0, buf[(r + 4) % 2], R, S, out);
+					CHECK(hipEventRecord(e1, 0));
+					CHECK(hipEventSynchronize(e1));
+					float ms;
+					CHECK(hipEventElapsedTime(&ms, e0, e1));
+					if (r >= 0) {
+						tot += ms;
+						best = ms < best ? ms : best;
+					}
+				}
+				printf("%s  {\"probe\": \"wgpool S%u\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f}", sep(), S,
+				       tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9);
+			}
 	}
 	if (all) {
 		// global pool with claims AHEAD steps ahead
