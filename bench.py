@@ -315,7 +315,7 @@ def main():
     if len(shards) > 1:
         line["shards_checked"] = shard_parity(shards, offs, sizes, rotate, P)
     if rank == 0 and world == 1 and len(shards) == 1 and launches:
-        probe = stream_probe("copy" if dsts else "read")
+        probe = stream_probe("copy" if dsts else "read", max(1, batch_bytes >> 20))
         if probe:
             line["roofline"]["probe"] = dict(probe, frac_of_probe=round(achieved_gbs / probe["GBps"], 4))
 
@@ -499,23 +499,24 @@ def sustain(shards, nstreams, seconds, sync_all, dist, backend, dev, torch):
     return elapsed, steps
 
 
-def stream_probe(kind):
-    """The same box's streaming ceiling for the kernel's access shape
-    (build/sched_probe, tools/sched_probe.hip: 1 GiB, 8-lane groups over
-    128-byte rows, 8 rows in flight per lane, nontemporal, one 1024-thread
-    workgroup per CU, equal static shares): "read" for the CRC kernel, "copy"
-    (read + write) for the fused CRC + copy.  None if the probe is missing."""
+def stream_probe(kind, mib):
+    """The same box's streaming ceiling for the kernel's access shape, at the
+    batch's size (build/sched_probe, tools/sched_probe.hip: `mib` MiB per
+    launch, 8-lane groups over 128-byte rows, 8 rows in flight per lane,
+    nontemporal, one 1024-thread workgroup per CU, equal static shares):
+    "read" for the CRC kernel, "copy" (read + write) for the fused CRC + copy.
+    None if the probe is missing."""
     exe = os.path.join(REPO, "build", "sched_probe")
     if not os.path.exists(exe):
         return None
-    r = subprocess.run([exe, "10", kind], capture_output=True, timeout=120)
+    r = subprocess.run([exe, "10", kind, str(mib)], capture_output=True, timeout=120)
     if r.returncode != 0:
         return None
     res = json.loads(r.stdout.decode())["results"][0]
     gbs = res.get("GBps_read_plus_write", res.get("GBps"))
-    return {"kind": kind, "GBps": gbs, "us_per_GiB": res["us"],
-            "what": "tools/sched_probe.hip: same access shape, nontemporal, static shares, 1 GiB" +
-                    (" read + 1 GiB written" if kind == "copy" else " read")}
+    return {"kind": kind, "GBps": gbs, "us_per_launch": res["us"],
+            "what": f"tools/sched_probe.hip: same access shape, nontemporal, static shares, {mib} MiB" +
+                    (f" read + {mib} MiB written" if kind == "copy" else " read") + " per launch"}
 
 
 def shard_parity(shards, offs, sizes, rotate, P):

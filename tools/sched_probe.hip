@@ -393,6 +393,37 @@ __global__ __launch_bounds__(1024, 1) void k_wgpool(const uint8_t *p, uint32_t R
 		out[w] = x;
 }
 
+// static shares, each wave's share read starting at a pseudo-random row of
+// it and wrapping around (ROT 1: one offset per wave, shared by its 8
+// groups; ROT 2: one offset per group): do the streams' aligned starts cost?
+template <int ROT>
+__global__ __launch_bounds__(1024, 1) void k_rot(const uint8_t *p, uint32_t R, uint32_t *out)
+{
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const PStep s = make_step(r0, r1 - r0, grp);
+	const uint32_t key = ROT == 1 ? w : w * 8u + grp;
+	const uint32_t off = s.n ? (key * 2654435761u >> 7) % s.n : 0u;
+	u32x4 acc = (u32x4)(0u), ring[D];
+	for (uint32_t r = 0; r < s.T; r += D) {
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			uint32_t q = min(r + i, s.n - 1u) + off;
+			q = q >= s.n ? q - s.n : q;
+			ring[i] = ld(p, s.row + q, g8);
+		}
+#pragma unroll
+		for (int i = 0; i < D; ++i)
+			if (r + i < s.n)
+				acc ^= ring[i];
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[w] = x;
+}
+
 // read+write copy, static shares, same shape
 __global__ __launch_bounds__(1024, 1) void k_copy(const uint8_t *p, uint8_t *q, uint32_t R)
 {
@@ -480,6 +511,32 @@ int main(int argc, char **argv)
 		}
 		printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"best_us\": %.2f, \"GBps\": %.1f, \"steals_last\": %u}",
 		       sep(), runs[k].name, tot / reps * 1e3, best * 1e3, bytes / (tot / reps * 1e-3) / 1e9, steals);
+	}
+	if (all || !strcmp(which, "rot")) {
+		for (int pass = 0; pass < 2; ++pass)
+			for (int mode = 0; mode < 3; ++mode) {
+				float tot = 0;
+				for (int r = -2; r < reps; ++r) {
+					CHECK(hipEventRecord(e0, 0));
+					const uint8_t *p = buf[(r + 4) % 2];
+					if (mode == 0)
+						hipLaunchKernelGGL(k_rot<0>, dim3(ncu), dim3(1024), 0, 0, p, R, out);
+					else if (mode == 1)
+						hipLaunchKernelGGL(k_rot<1>, dim3(ncu), dim3(1024), 0, 0, p, R, out);
+					else
+						hipLaunchKernelGGL(k_rot<2>, dim3(ncu), dim3(1024), 0, 0, p, R, out);
+					CHECK(hipEventRecord(e1, 0));
+					CHECK(hipEventSynchronize(e1));
+					float ms;
+					CHECK(hipEventElapsedTime(&ms, e0, e1));
+					if (r >= 0)
+						tot += ms;
+				}
+				static const char *nm[] = {"static, no rotation (no prefetch ring)", "rotated per wave",
+							   "rotated per group"};
+				printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}", sep(), nm[mode], tot / reps * 1e3,
+				       bytes / (tot / reps * 1e-3) / 1e9);
+			}
 	}
 	if (all || !strcmp(which, "wgpool")) {
 		// workgroup pools: items of S rows claimed through LDS
