@@ -453,3 +453,32 @@ def test_internal_workspace_two_streams(torch_dev, P):
     for buf, offs, L, k, descs, out, st in jobs:
         want = O.crcs(buf.cpu().numpy(), offs, [L] * len(offs), [k] * len(offs))
         assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+def test_max_length_buffer(torch_dev, P):
+    # the longest buffer the C-ABI can describe (unsigned int length:
+    # 2^32 - 1 bytes) at an odd address, beside an empty and a 1-byte buffer;
+    # 33.5 M rows in one buffer, split over every wave of the chip
+    torch, dev = torch_dev
+    n = (1 << 32) - 1
+    buf = torch.randint(0, 256, (n + 64,), dtype=torch.uint8, device=dev)
+    base = buf.data_ptr()
+    seeds = [0x9E3779B9, 7, 0xFFFFFFFF]
+    descs = P.make_descs([base + 5, base + 3, base + n + 10], [n, 0, 1], seeds, device=dev)
+    out = torch.zeros(3, dtype=torch.int32, device=dev)
+    P.dev_batch_async(descs, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    host = buf.cpu().numpy()
+    H = O.hw()
+    if H is not None:  # SSE4.2 restatement (bit-exact vs the reference, tests/test_oracle.py)
+        want0 = H.hw_crc32c(seeds[0], host.ctypes.data + 5, n)
+        # and the byte-loop oracle on the last 64 MiB, through the chaining law
+        head = H.hw_crc32c(seeds[0], host.ctypes.data + 5, n - (64 << 20))
+        tail = O.crc(0, host[5 + n - (64 << 20):5 + n])
+        assert P.crc32c_combine(head, tail, 64 << 20) == want0
+    else:
+        want0 = O.crc(seeds[0], host[5:5 + n])
+    assert int(got[0]) == want0
+    assert int(got[1]) == seeds[1]
+    assert int(got[2]) == O.crc(seeds[2], host[n + 10:n + 11])
