@@ -131,7 +131,7 @@ __device__ __forceinline__ PStep steal(uint64_t *ctl, uint32_t W, uint32_t w, ui
 	return none;
 }
 
-template <int MODE> // 0 static, 1 claims, 2 steal
+template <int MODE> // 0 static, 1 claims, 2 steal, 3 static in steps of S rows (no atomics)
 __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R, uint64_t *ctl, uint32_t S,
 						    uint32_t *out, uint32_t *nsteal)
 {
@@ -141,8 +141,13 @@ __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R,
 	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
 	u32x4 acc = (u32x4)(0u), ring[D];
 	PStep cur;
+	uint32_t next_r = r0;
 	if (MODE == 0) {
 		cur = make_step(r0, r1 - r0, grp); // the whole share is one step
+	} else if (MODE == 3) {
+		const uint32_t n0 = min(S, r1 - r0);
+		cur = make_step(r0, n0, grp);
+		next_r = r0 + n0;
 	} else {
 		const uint32_t n0 = min(S, r1 - r0);
 		if (lane == 0)
@@ -157,7 +162,7 @@ __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R,
 	while (cur.T) {
 		// claim the step after this one now: consumed at this step's end
 		uint64_t fut = 0;
-		if (MODE != 0 && lane == 0)
+		if (MODE != 0 && MODE != 3 && lane == 0)
 			fut = __hip_atomic_fetch_add(ctl + w, (uint64_t)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		const uint32_t nblk = (cur.T + D - 1) / D;
 		uint32_t blk = 0;
@@ -173,7 +178,12 @@ __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R,
 		PStep nxt;
 		nxt.T = 0;
 		nxt.row = nxt.n = 0;
-		if (MODE != 0) {
+		if (MODE == 3) {
+			if (next_r < r1) {
+				nxt = make_step(next_r, min(S, r1 - next_r), grp);
+				next_r += min(S, r1 - next_r);
+			}
+		} else if (MODE != 0) {
 			fut = __shfl(fut, 0);
 			const uint32_t b = uni((uint32_t)fut), e = uni((uint32_t)(fut >> 32));
 			if (b < e)
@@ -480,11 +490,14 @@ int main(int argc, char **argv)
 		const char *name;
 		int mode;
 		uint32_t S;
-	} runs[] = {{"static", 0, 0},     {"claims S256", 1, 256}, {"steal S256", 2, 256}, {"steal S128", 2, 128},
-		    {"steal S64", 2, 64}, {"claims S128", 1, 128}, {"static (again)", 0, 0}};
+	} runs[] = {{"static", 0, 0},         {"claims S256", 1, 256},  {"steal S256", 2, 256},
+		    {"steal S128", 2, 128},     {"steal S64", 2, 64},     {"claims S128", 1, 128},
+		    {"static steps S256", 3, 256}, {"static steps S128", 3, 128}, {"static (again)", 0, 0}};
 	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, ncu, bytes);
 	for (size_t k = 0; k < sizeof(runs) / sizeof(runs[0]); ++k) {
-		if (only_copy || (!all && runs[k].mode != 0) || (!all && !only_read))
+		const bool steps_mode = !strcmp(which, "steps");
+		if (only_copy || (!all && !only_read && !steps_mode) || (only_read && runs[k].mode != 0) ||
+		    (steps_mode && runs[k].mode != 0 && runs[k].mode != 3))
 			continue;
 		float tot = 0, best = 1e9f;
 		uint32_t steals = 0;
@@ -497,6 +510,8 @@ int main(int argc, char **argv)
 				hipLaunchKernelGGL(k_sched<0>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			else if (runs[k].mode == 1)
 				hipLaunchKernelGGL(k_sched<1>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
+			else if (runs[k].mode == 3)
+				hipLaunchKernelGGL(k_sched<3>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			else
 				hipLaunchKernelGGL(k_sched<2>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			CHECK(hipEventRecord(e1, 0));
