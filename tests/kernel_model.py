@@ -56,8 +56,9 @@ def size_class(rows):
 
 def plan(descs, rng=None):
     """descs: list of (addr, len).  Returns per-slot cores, lrs, partials,
-    nzs.  Order inside a size class is arbitrary on the GPU (LDS atomics);
-    `rng` shuffles it to cover that."""
+    nzs.  Without `rng`, the plan kernel's order (stable by class, 16-blocks
+    interleaved below the split size); with `rng`, an arbitrary order inside
+    each class (the main kernel must not depend on it)."""
     n = len(descs)
     nch = (n + CHUNK - 1) // CHUNK
     cores = [None] * (nch * CHUNK)
@@ -81,6 +82,14 @@ def plan(descs, rng=None):
             group = [it for it in items if it["cls"] == cls]
             if rng is not None:
                 rng.shuffle(group)
+            elif group and group[0]["rows"] < SPLIT:
+                # the plan kernel's order: stable inside the class, and inside
+                # every full block of 16 ranks 0,2,..,14 then 1,3,..,15
+                g2 = list(group)
+                for k in range(0, len(group) - 15, 16):
+                    blk = group[k:k + 16]
+                    g2[k:k + 16] = blk[0::2] + blk[1::2]
+                group = g2
             order += group
         acc = 0
         for pos in range(CHUNK):

@@ -131,7 +131,21 @@ __device__ __forceinline__ PStep steal(uint64_t *ctl, uint32_t W, uint32_t w, ui
 	return none;
 }
 
-template <int MODE> // 0 static, 1 claims, 2 steal, 3 static in steps of S rows (no atomics)
+// MODE 4: like 3, but the wave's share is cut the other way: step j gives
+// group g rows [r0 + g * (share / 8) + j * S / 8, + S / 8) -- every group
+// walks ONE contiguous range of the share across the steps (as 2 consecutive
+// 4 KiB buffers per group would), instead of a fresh 32-row block per step.
+__device__ __forceinline__ PStep make_step_cols(uint32_t r0, uint32_t share, uint32_t j, uint32_t S, uint32_t grp)
+{
+	PStep s;
+	const uint32_t per = share / 8u, k = S / 8u;
+	s.row = r0 + grp * per + j * k;
+	s.n = min(k, per - min(per, j * k));
+	s.T = s.n ? k : 0u;
+	return s;
+}
+
+template <int MODE> // 0 static, 1 claims, 2 steal, 3 static in steps of S rows (no atomics), 4 see above
 __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R, uint64_t *ctl, uint32_t S,
 						    uint32_t *out, uint32_t *nsteal)
 {
@@ -148,6 +162,9 @@ __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R,
 		const uint32_t n0 = min(S, r1 - r0);
 		cur = make_step(r0, n0, grp);
 		next_r = r0 + n0;
+	} else if (MODE == 4) {
+		cur = make_step_cols(r0, r1 - r0, 0, S, grp);
+		next_r = 1; // next step index
 	} else {
 		const uint32_t n0 = min(S, r1 - r0);
 		if (lane == 0)
@@ -162,7 +179,7 @@ __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R,
 	while (cur.T) {
 		// claim the step after this one now: consumed at this step's end
 		uint64_t fut = 0;
-		if (MODE != 0 && MODE != 3 && lane == 0)
+		if (MODE != 0 && MODE != 3 && MODE != 4 && lane == 0)
 			fut = __hip_atomic_fetch_add(ctl + w, (uint64_t)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		const uint32_t nblk = (cur.T + D - 1) / D;
 		uint32_t blk = 0;
@@ -183,6 +200,9 @@ __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R,
 				nxt = make_step(next_r, min(S, r1 - next_r), grp);
 				next_r += min(S, r1 - next_r);
 			}
+		} else if (MODE == 4) {
+			nxt = make_step_cols(r0, r1 - r0, next_r++, S, grp);
+			nxt.T = uni(nxt.T);
 		} else if (MODE != 0) {
 			fut = __shfl(fut, 0);
 			const uint32_t b = uni((uint32_t)fut), e = uni((uint32_t)(fut >> 32));
@@ -492,12 +512,13 @@ int main(int argc, char **argv)
 		uint32_t S;
 	} runs[] = {{"static", 0, 0},         {"claims S256", 1, 256},  {"steal S256", 2, 256},
 		    {"steal S128", 2, 128},     {"steal S64", 2, 64},     {"claims S128", 1, 128},
-		    {"static steps S256", 3, 256}, {"static steps S128", 3, 128}, {"static (again)", 0, 0}};
+		    {"static steps S256", 3, 256}, {"static steps S128", 3, 128}, {"column steps S256", 4, 256},
+		    {"column steps S128", 4, 128}, {"static (again)", 0, 0}};
 	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, ncu, bytes);
 	for (size_t k = 0; k < sizeof(runs) / sizeof(runs[0]); ++k) {
 		const bool steps_mode = !strcmp(which, "steps");
 		if (only_copy || (!all && !only_read && !steps_mode) || (only_read && runs[k].mode != 0) ||
-		    (steps_mode && runs[k].mode != 0 && runs[k].mode != 3))
+		    (steps_mode && runs[k].mode != 0 && runs[k].mode != 3 && runs[k].mode != 4))
 			continue;
 		float tot = 0, best = 1e9f;
 		uint32_t steals = 0;
@@ -512,6 +533,8 @@ int main(int argc, char **argv)
 				hipLaunchKernelGGL(k_sched<1>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			else if (runs[k].mode == 3)
 				hipLaunchKernelGGL(k_sched<3>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
+			else if (runs[k].mode == 4)
+				hipLaunchKernelGGL(k_sched<4>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			else
 				hipLaunchKernelGGL(k_sched<2>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			CHECK(hipEventRecord(e1, 0));
