@@ -64,10 +64,8 @@
 #define L_TAB32 (L_TAB16 + 4096u)
 #define L_TAB64 (L_TAB32 + 4096u)
 #define L_POWB (L_TAB64 + 4096u) // 1536 B
-#define L_CHUNK (L_POWB + 1536u) // 4 KiB: chunk row offsets
-#define L_NZ (L_CHUNK + 4096u)   // 4 KiB: chunk non-empty counts
-#define L_MISC (L_NZ + 4096u)    // scan scratch
-#define L_DEFER (L_MISC + 128u)  // 512 B: split-step results, keyed by output slot
+#define L_NZ (L_POWB + 1536u)    // 4 KiB: chunk non-empty counts
+#define L_DEFER (L_NZ + 4096u)   // 512 B: split-step results, keyed by output slot
 #define L_DEFER_DONE (L_DEFER + 8u * PECH_DEFER_SLOTS) // waves of the workgroup done
 #define L_BYTES (L_DEFER_DONE + 16u)
 static_assert(L_BYTES <= 160u * 1024u, "main kernel LDS over 160 KiB");
@@ -456,50 +454,6 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 #define LD_PIECE(S, a, tag) (__builtin_nontemporal_load((g_u32x4 *)(a)))
 #endif
 
-// Locate row r of the batch's row space in ONE global round: the chunk by
-// binary search of the LDS prefix, then the whole wave reads the chunk's
-// PECH_CHUNK row offsets (16 per lane, four 16-byte loads) and counts those
-// <= the chunk-local row (they are nondecreasing, strictly over the chunk's
-// nz non-empty cores).  Returns the position (plan order) and the row inside
-// that buffer, wave-uniform.
-static_assert(PECH_CHUNK == 64u * 16u, "find_start_wave: 16 row offsets per lane");
-__device__ __forceinline__ void find_start_wave(const uint32_t *__restrict__ lrs, const uint32_t *lds,
-						uint32_t nchunks, uint32_t r, uint32_t lane, uint32_t &pos,
-						uint32_t &lr)
-{
-	uint32_t clo = 0, chi = nchunks;
-	while (chi - clo > 1) {
-		const uint32_t mid = (clo + chi) >> 1;
-		if (lds[L_CHUNK / 4u + mid] <= r)
-			clo = mid;
-		else
-			chi = mid;
-	}
-	const uint32_t rr = r - lds[L_CHUNK / 4u + clo];
-	const uint32_t nz = lds[L_NZ / 4u + clo];
-	const u32x4 *src = (const u32x4 *)(lrs + clo * PECH_CHUNK + lane * 16u);
-	uint32_t cnt = 0, lo = 0;
-#pragma unroll
-	for (uint32_t k = 0; k < 4; ++k) {
-		const u32x4 v = src[k];
-		const uint32_t i0 = lane * 16u + 4u * k;
-		const uint32_t e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-		for (uint32_t j = 0; j < 4; ++j) {
-			const bool ok = i0 + j < nz && e[j] <= rr;
-			cnt += ok ? 1u : 0u;
-			lo = ok ? max(lo, e[j]) : lo;
-		}
-	}
-#pragma unroll
-	for (uint32_t d = 1; d < 64; d <<= 1) {
-		cnt += __shfl_xor(cnt, d);
-		lo = max(lo, (uint32_t)__shfl_xor(lo, d));
-	}
-	pos = uni(clo * PECH_CHUNK + cnt - 1u);
-	lr = uni(rr - lo);
-}
-
 static_assert(PECH_MAIN_WAVES % 4 == 0 && PECH_MAIN_WAVES <= 16, "waves per workgroup: 4, 8, 12 or 16");
 
 // Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
@@ -765,12 +719,23 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 {
 	const uint32_t tid = threadIdx.x;
 	STAMP(t_entry);
+	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
+	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
+	const uint32_t wave = uni(tid >> 6);
+	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 
-	// Table constants first: their loads (L2/MALL) overlap the chunk-count
-	// loads below, and the LDS fill is done before the scan's barriers --
-	// issued after the ring prime they would queue behind its HBM loads
-	// (vmcnt is in order; measured 4 us of prologue).
+	// Prologue (v0.11): three dependent global rounds before the first data
+	// instead of four, and no barrier until the ring is primed.  Every wave
+	// issues at entry, all in flight together:
+	//   the table constants (written to LDS only after the prime, from
+	//   registers: issued first, their wait never drains the ring),
+	//   every chunk's row total and non-empty count (16 chunks per lane: the
+	//   wave scans them itself -- no workgroup scan, no barrier),
+	//   the row offsets of the chunk it most likely starts in (speculative:
+	//   exact for one chunk and for uniform batches; reloaded if wrong).
 	static_assert(1024u % PECH_MAIN_THREADS == 0u, "table fill: A_128 words split evenly over the threads");
+	static_assert(PECH_MAX_CHUNKS == 64u * 16u, "wave scan: 16 chunks per lane");
+	static_assert(PECH_CHUNK == 64u * 16u, "find: 16 row offsets per lane");
 	constexpr uint32_t T128 = 1024u / PECH_MAIN_THREADS; // A_128 words per thread
 	constexpr uint32_t NT4 = (PECH_C_TAB1 - PECH_C_TAB4) / 4u; // single-copy tables, 16-B words
 	constexpr uint32_t TPT = (NT4 + PECH_MAIN_THREADS - 1u) / PECH_MAIN_THREADS;
@@ -782,71 +747,44 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	u32x4 tv[TPT];
 #pragma unroll
 	for (uint32_t k = 0; k < TPT; ++k)
-		tv[k] = tid + k * PECH_MAIN_THREADS < NT4 ? c4[tid + k * PECH_MAIN_THREADS] : (u32x4)(0u);
-
-	// chunk row offsets, non-empty counts and the batch's total row count
-	uint32_t Rtot;
-	{
-		// each thread owns CPT consecutive chunks
-		constexpr uint32_t CPT = (PECH_MAX_CHUNKS + PECH_MAIN_THREADS - 1) / PECH_MAIN_THREADS;
-		uint32_t pv[CPT], nv[CPT], sum = 0;
+		tv[k] = c4[min(tid + k * PECH_MAIN_THREADS, NT4 - 1u)];
+	// (partials / nzs hold PECH_MAX_CHUNKS entries: whole-array loads are in bounds)
+	u32x4 pv4[4], nv4[4], lr4[4];
 #pragma unroll
-		for (uint32_t k = 0; k < CPT; ++k) {
-			const uint32_t c = tid * CPT + k;
-			pv[k] = c < nchunks ? partials[c] : 0u;
-			nv[k] = c < nchunks ? nzs[c] : 0u;
-		}
-		// A_128 once per bank: its 32 copies as 8 x 16 B; lane t starts at
-		// copy group t mod 8 so neighbouring lanes, whose rows are 256 B
-		// apart, write different banks.  Then the single-copy tables.
-#pragma unroll
-		for (uint32_t j = 0; j < T128; ++j) {
-			const uint32_t w = tid + j * PECH_MAIN_THREADS, k = w >> 8, e = w & 0xFFu;
-			const u32x4 v = (u32x4)(t128[j]);
-			char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
-#pragma unroll
-			for (uint32_t q = 0; q < 8u; ++q)
-				*(u32x4 *)(dst + 16u * ((q + w) & 7u)) = v;
-		}
-#pragma unroll
-		for (uint32_t k = 0; k < TPT; ++k)
-			if (tid + k * PECH_MAIN_THREADS < NT4)
-				*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
-		if (tid < PECH_DEFER_SLOTS) { // empty deferral table (published by the scan's barriers)
-			lds[L_DEFER / 4u + tid] = PECH_DEFER_EMPTY;
-			lds[L_DEFER / 4u + PECH_DEFER_SLOTS + tid] = 0u;
-			if (tid == 0)
-				lds[L_DEFER_DONE / 4u] = 0u;
-		}
-#pragma unroll
-		for (uint32_t k = 0; k < CPT; ++k) {
-			const uint32_t c = tid * CPT + k;
-			if (c < PECH_MAX_CHUNKS)
-				lds[L_NZ / 4u + c] = nv[k];
-			sum += pv[k];
-		}
-		uint32_t ex = block_excl_scan<PECH_MAIN_THREADS>(sum, lds + L_MISC / 4u, &Rtot); // (barriers inside)
-#pragma unroll
-		for (uint32_t k = 0; k < CPT; ++k) {
-			if (tid * CPT + k < PECH_MAX_CHUNKS)
-				lds[L_CHUNK / 4u + tid * CPT + k] = ex;
-			ex += pv[k];
-		}
+	for (uint32_t k = 0; k < 4; ++k) {
+		pv4[k] = ((const u32x4 *)partials)[lane * 4u + k];
+		nv4[k] = ((const u32x4 *)nzs)[lane * 4u + k];
 	}
-	__syncthreads();
+	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
+	const uint32_t cg = uni((uint32_t)((uint64_t)wglob * nchunks / W)); // likely start chunk
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k)
+		lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + lane * 16u))[k];
+
+	// the wave's own exclusive scan of the chunk totals
+	uint32_t pc[16], nc[16], lsum = 0;
+#pragma unroll
+	for (uint32_t k = 0; k < 16; ++k) {
+		const bool real = lane * 16u + k < nchunks;
+		pc[k] = real ? pv4[k >> 2][k & 3u] : 0u;
+		nc[k] = real ? nv4[k >> 2][k & 3u] : 0u;
+		lsum += pc[k];
+	}
+	uint32_t incl = lsum;
+#pragma unroll
+	for (uint32_t d = 1; d < 64; d <<= 1) {
+		const uint32_t y = __shfl_up(incl, d);
+		if (lane >= d)
+			incl += y;
+	}
+	const uint32_t Rtot = uni(__shfl(incl, 63));
 	STAMP(t_scan);
-	Rtot = uni(Rtot);
 	// Every wave gets an equal share of the batch's rows (at least rpw_min).
-	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 	const uint32_t rpw_eq = (uint32_t)(((uint64_t)Rtot + W - 1u) / W);
 	const uint32_t rpw = max(rpw_min, rpw_eq);
 	const uint64_t wg0 = (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
 	if (wg0 >= Rtot)
 		return; // whole workgroup idle (small batch)
-
-	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
-	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
-	const uint32_t wave = uni(tid >> 6);
 	u32x4 ring[U];
 	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
 	// equal contiguous pieces (age-weighted shares measured no better,
@@ -855,20 +793,95 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
 	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
 	const uint32_t rem_all = r1 - r0;
+
+	// nz table for plan_step: every wave writes all of it (the same values)
+	// and reads back only its own writes until the barrier below
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k)
+		*(u32x4 *)(lds + L_NZ / 4u + lane * 16u + 4u * k) =
+			u32x4{nc[4 * k], nc[4 * k + 1], nc[4 * k + 2], nc[4 * k + 3]}; // braces: a parenthesised list is a comma splat
+
 	uint32_t p0 = 0, lr0 = 0;
-	if (rem_all)
-		find_start_wave(lrs, lds, nchunks, r0, lane, p0, lr0);
+	if (rem_all) {
+		// start chunk j: the last chunk whose prefix is <= r0 (non-empty,
+		// since r0 < Rtot); its prefix and non-empty count
+		uint32_t pre = incl - lsum, cnt = 0, pj = 0, nzj = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 16; ++k) {
+			const bool le = lane * 16u + k < nchunks && pre <= r0;
+			cnt += le ? 1u : 0u;
+			pj = le ? pre : pj;
+			nzj = le ? nc[k] : nzj;
+			pre += pc[k];
+		}
+		uint32_t jc = cnt;
+#pragma unroll
+		for (uint32_t d = 1; d < 64; d <<= 1)
+			jc += __shfl_xor(jc, d);
+		const uint32_t j = uni(jc) - 1u;
+		pj = uni(__shfl(pj, j >> 4));
+		nzj = uni(__shfl(nzj, j >> 4));
+		const uint32_t rr = r0 - pj;
+		if (j != cg) { // speculation missed: the start chunk's row offsets now
+#pragma unroll
+			for (uint32_t k = 0; k < 4; ++k)
+				lr4[k] = ((const u32x4 *)(lrs + j * PECH_CHUNK + lane * 16u))[k];
+		}
+		// position: the count of the chunk's offsets <= rr (nondecreasing
+		// over its nz non-empty cores), and the row inside that buffer
+		uint32_t c2 = 0, lo = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 16; ++k) {
+			const uint32_t e = lr4[k >> 2][k & 3u];
+			const bool ok = lane * 16u + k < nzj && e <= rr;
+			c2 += ok ? 1u : 0u;
+			lo = ok ? max(lo, e) : lo;
+		}
+#pragma unroll
+		for (uint32_t d = 1; d < 64; d <<= 1) {
+			c2 += __shfl_xor(c2, d);
+			lo = max(lo, (uint32_t)__shfl_xor(lo, d));
+		}
+		p0 = uni(j * PECH_CHUNK + c2 - 1u);
+		lr0 = uni(rr - lo);
+#ifdef PECH_DEBUG_BOUNDS
+		if (lane == 0 && (j >= nchunks || c2 == 0 || c2 > nzj || lr0 >= cores[p0].rows))
+			printf("PECH OOB prologue blk %u wave %u r0 %u j %u cg %u nchunks %u nzj %u c2 %u rr %u lo %u rows %u\n",
+			       blockIdx.x, wave, r0, j, cg, nchunks, nzj, c2, rr, lo, cores[min(p0, nchunks * PECH_CHUNK - 1u)].rows);
+#endif
+	}
 	STAMP(t_find);
 	Step S = plan_step<COPY>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp);
 	STAMP(t_plan);
 	if (S.T)
 		RING_PRIME(S, ring);
 
+	// The LDS tables, needed from the first row on, written while the prime
+	// is in flight.  A_128 once per bank: its 32 copies as 8 x 16 B; lane t
+	// starts at copy group t mod 8 so neighbouring lanes, whose rows are
+	// 256 B apart, write different banks.  Then the single-copy tables and
+	// the empty deferral table.
+#pragma unroll
+	for (uint32_t j = 0; j < T128; ++j) {
+		const uint32_t w = tid + j * PECH_MAIN_THREADS, k = w >> 8, e = w & 0xFFu;
+		const u32x4 v = (u32x4)(t128[j]);
+		char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+#pragma unroll
+		for (uint32_t q = 0; q < 8u; ++q)
+			*(u32x4 *)(dst + 16u * ((q + w) & 7u)) = v;
+	}
+#pragma unroll
+	for (uint32_t k = 0; k < TPT; ++k)
+		if (tid + k * PECH_MAIN_THREADS < NT4)
+			*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
+	if (tid < PECH_DEFER_SLOTS) {
+		lds[L_DEFER / 4u + tid] = PECH_DEFER_EMPTY;
+		lds[L_DEFER / 4u + PECH_DEFER_SLOTS + tid] = 0u;
+		if (tid == 0)
+			lds[L_DEFER_DONE / 4u] = 0u;
+	}
 	STAMP(t_fill);
-	// No barrier here: the LDS tables were written before the scan's
-	// barriers, and the ring is the wave's own.  Each wave starts streaming
-	// as soon as its prime is issued (a barrier cost 1-2 us of prologue).
-
+	__syncthreads(); // tables published; every wave's prime is already in flight
 	STAMP(t_start);
 #ifdef PECH_STAMPS
 	uint64_t tq[3] = {0, 0, 0};
@@ -926,6 +939,16 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
 			st_piece<COPY>(S, r + i, ring[i], r + i < S.nu);
 		}
+#ifdef PECH_DEBUG_BOUNDS
+		{ // debug build: an active group's output slot must lie in this launch's slots
+			const bool bad = S.nu != 0 && STEP_ORIG(S) >= nchunks * PECH_CHUNK;
+			if (bad && g8 == 0)
+				printf("PECH OOB out blk %u wave %u orig %u nu %u T %u pos %u\n", blockIdx.x, wave, STEP_ORIG(S), S.nu,
+				       S.T, S.pos);
+			if (bad)
+				S.nu = 0;
+		}
+#endif
 		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));
 		S = N;
 #ifdef PECH_STAMPS
@@ -946,7 +969,14 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		static_assert(PECH_DEFER_SLOTS == 64u, "one slot per lane of the flushing wave");
 		if (done == PECH_MAIN_WAVES - 1u) {
 			const uint32_t k = lds[L_DEFER / 4u + lane];
-			if (k != PECH_DEFER_EMPTY)
+			bool flush = k != PECH_DEFER_EMPTY;
+#ifdef PECH_DEBUG_BOUNDS
+			if (flush && k >= nchunks * PECH_CHUNK) {
+				printf("PECH OOB flush blk %u slot %u key %u\n", blockIdx.x, lane, k);
+				flush = false;
+			}
+#endif
+			if (flush)
 				atomicXor(out + k, lds[L_DEFER / 4u + PECH_DEFER_SLOTS + lane]);
 		}
 	}

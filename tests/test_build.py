@@ -178,3 +178,17 @@ def test_row_addr_launder_survives(device_asm):
                 if any(x.startswith("global_load_dwordx4") for x in nxt):
                     fed += 1
         assert fed >= 4, (kernel, fed, n)
+
+
+def test_no_comma_vector_casts():
+    """`(u32x4)(a, b, c, d)` is a C++ comma expression: it splats `d`, it is
+    not a vector literal (OpenCL's meaning).  v0.11's prologue wrote its
+    per-chunk non-empty counts that way and plan_step then walked past the
+    chunk (a GPU fault in the async tests).  Vector literals take braces."""
+    pat = re.compile(r"\((?:u32x4|g_u32x4|uint4|u64x2)\)\s*\(([^()]|\([^()]*\))*,")
+    for d in ("pech_amd/csrc", "tools"):
+        for f in os.listdir(os.path.join(REPO, d)):
+            if f.endswith((".hip", ".cpp", ".h")):
+                src = open(os.path.join(REPO, d, f)).read()
+                bad = [l for l in src.split("\n") if pat.search(l.split("//")[0])]
+                assert not bad, (f, bad)

@@ -156,7 +156,12 @@ __global__ __launch_bounds__(1024, 1) void k_sched(const uint8_t *p, uint32_t R,
 	u32x4 acc = (u32x4)(0u), ring[D];
 	PStep cur;
 	uint32_t next_r = r0;
-	if (MODE == 0) {
+	if (MODE == 5) { // static, after an idle prologue of about S microseconds (s_memrealtime: 100 MHz)
+		const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+		while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * S)
+			__builtin_amdgcn_s_sleep(8);
+	}
+	if (MODE == 0 || MODE == 5) {
 		cur = make_step(r0, r1 - r0, grp); // the whole share is one step
 	} else if (MODE == 3) {
 		const uint32_t n0 = min(S, r1 - r0);
@@ -513,12 +518,14 @@ int main(int argc, char **argv)
 	} runs[] = {{"static", 0, 0},         {"claims S256", 1, 256},  {"steal S256", 2, 256},
 		    {"steal S128", 2, 128},     {"steal S64", 2, 64},     {"claims S128", 1, 128},
 		    {"static steps S256", 3, 256}, {"static steps S128", 3, 128}, {"column steps S256", 4, 256},
-		    {"column steps S128", 4, 128}, {"static (again)", 0, 0}};
+		    {"column steps S128", 4, 128}, {"static after 3 us idle", 5, 3}, {"static after 6 us idle", 5, 6},
+		    {"static (again)", 0, 0}};
 	printf("{\"device\": \"%s\", \"cus\": %d, \"bytes\": %zu, \"results\": [\n", prop.name, ncu, bytes);
 	for (size_t k = 0; k < sizeof(runs) / sizeof(runs[0]); ++k) {
-		const bool steps_mode = !strcmp(which, "steps");
-		if (only_copy || (!all && !only_read && !steps_mode) || (only_read && runs[k].mode != 0) ||
-		    (steps_mode && runs[k].mode != 0 && runs[k].mode != 3 && runs[k].mode != 4))
+		const int md = runs[k].mode;
+		const bool pick = all || (only_read && md == 0) || (!strcmp(which, "steps") && (md == 0 || md == 3 || md == 4)) ||
+				  (!strcmp(which, "idle") && (md == 0 || md == 5));
+		if (!pick)
 			continue;
 		float tot = 0, best = 1e9f;
 		uint32_t steals = 0;
@@ -535,6 +542,8 @@ int main(int argc, char **argv)
 				hipLaunchKernelGGL(k_sched<3>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			else if (runs[k].mode == 4)
 				hipLaunchKernelGGL(k_sched<4>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
+			else if (runs[k].mode == 5)
+				hipLaunchKernelGGL(k_sched<5>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			else
 				hipLaunchKernelGGL(k_sched<2>, dim3(ncu), dim3(1024), 0, 0, p, R, ctl, runs[k].S, out, nsteal);
 			CHECK(hipEventRecord(e1, 0));
