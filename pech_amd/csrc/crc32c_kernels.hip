@@ -88,18 +88,40 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v)
 	return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
+// Inclusive add-scan over the 64 lanes by DPP moves (no LDS round trips, which
+// is what __shfl_up compiles to: ds_bpermute): Hillis-Steele inside each
+// 16-lane row (row_shr 1, 2, 4, 8 with zero fill), then row 15's sum into
+// rows 1 and 3 (row_bcast:15) and lane 31's into rows 2 and 3 (row_bcast:31).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+	return x;
+}
+
+// The last lane with a nonzero `c`, for lane values that are a monotone
+// prefix (every lane before it nonzero): a ballot instead of a reduction.
+__device__ __forceinline__ uint32_t last_lane_with(uint32_t c)
+{
+	const uint64_t m = __ballot(c != 0u);
+	return 63u - (uint32_t)__builtin_clzll(m | 1ull);
+}
+
+__device__ __forceinline__ uint32_t lane_value(uint32_t v, uint32_t lane)
+{
+	return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
 // NT-thread exclusive scan; scratch = NT/64 LDS words
 template <uint32_t NT = PECH_WG_THREADS>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t *total)
 {
 	const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-	uint32_t x = v;
-#pragma unroll
-	for (uint32_t d = 1; d < 64; d <<= 1) {
-		const uint32_t y = __shfl_up(x, d);
-		if (lane >= d)
-			x += y;
-	}
+	const uint32_t x = wave_incl_scan(v);
 	if (lane == 63u)
 		scratch[wave] = x;
 	__syncthreads();
@@ -458,10 +480,12 @@ static_assert(PECH_MAIN_WAVES % 4 == 0 && PECH_MAIN_WAVES <= 16, "waves per work
 
 // Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
 // the destination offset of each group's buffer (deltas[orig], scalar loads).
-template <bool COPY>
+// PRE: `pre` holds cores[ppos + grp] (loaded at kernel entry); a step that
+// starts at ppos takes its descriptors from it instead of loading them.
+template <bool COPY, bool PRE = false>
 __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
 					  const uint32_t *lds, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
-					  uint32_t g8, uint32_t grp)
+					  uint32_t g8, uint32_t grp, const pech_core &pre = pech_core{}, uint32_t ppos = 0)
 {
 	Step S;
 	int64_t dl = 0;
@@ -484,7 +508,16 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			pos = (c + 1u) << 10;
 			continue;
 		}
-		const pech_core cd = cores[pos];
+		const bool hit = PRE && pos == ppos; // wave-uniform
+		pech_core cd;
+		if (hit)
+			cd = pre; // lanes 0-7 (group 0) hold cores[pos]; uni() reads lane 0
+		else
+			cd = cores[pos];
+#ifdef PECH_DEBUG_BOUNDS
+		if (hit && (cd.rows != cores[pos + grp].rows || cd.vbase != cores[pos + grp].vbase))
+			printf("PECH OOB preloaded descriptor pos %u grp %u\n", pos, grp);
+#endif
 		const uint32_t rows0 = uni(cd.rows);
 		const uint64_t vb0 = uni64(cd.vbase);
 		const uint32_t meta0 = uni(cd.meta);
@@ -524,6 +557,17 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			// workspace memory); such entries are never used.
 			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
 			int64_t mdl = 0;
+			if (hit) {
+				vlo = (uint32_t)pre.vbase;
+				vhi = (uint32_t)(pre.vbase >> 32);
+				mrows = pre.rows;
+				mmeta = pre.meta;
+				if (COPY) {
+					const uint32_t pj = pos + grp;
+					const bool okj = (pj & 1023u) < nzc && (pj >> 10) == c;
+					mdl = deltas[okj ? PECH_META_ORIG(pre.meta) : 0u];
+				}
+			} else {
 #pragma unroll
 			for (uint32_t j = 0; j < 8; ++j) {
 				const pech_core dj = cores[pos + j];
@@ -540,6 +584,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 					mdl = mine ? dj_dl : mdl;
 				}
 			}
+			}
 			pech_core my;
 			my.vbase = ((uint64_t)vhi << 32) | vlo;
 			my.rows = mrows;
@@ -553,28 +598,22 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			const uint32_t kcut = cutm ? (uint32_t)(__builtin_ctzll(cutm) >> 3) : 8u;
 			const uint32_t mylr = grp ? 0u : lr;
 			const uint32_t avail = grp < kcut ? myrows - mylr : 0u;
-			// exclusive prefix of avail over groups (lanes 8j)
-			uint32_t pre = avail, x;
-			x = __shfl_up(pre, 8);
-			if (lane >= 8)
-				pre += x;
-			x = __shfl_up(pre, 16);
-			if (lane >= 16)
-				pre += x;
-			x = __shfl_up(pre, 32);
-			if (lane >= 32)
-				pre += x;
-			pre -= avail;
+			// exclusive prefix of avail over groups (one contribution per
+			// group, from its lane 0), by DPP: no LDS round trips
+			const uint32_t incl = wave_incl_scan(g8 == 0 ? avail : 0u);
+			const uint32_t pre = incl - avail;
 			const uint32_t nu = pre >= rem ? 0u : min(avail, rem - pre);
-			uint32_t tmax = nu, tmin = nu ? nu : 0xFFFFFFFFu;
+			// the step's longest and shortest run: 8 lane reads (group-uniform values)
+			uint32_t tmax = 0, tmin = 0xFFFFFFFFu;
 #pragma unroll
-			for (uint32_t d = 8; d < 64; d <<= 1) {
-				tmax = max(tmax, (uint32_t)__shfl_xor(tmax, d));
-				tmin = min(tmin, (uint32_t)__shfl_xor(tmin, d));
+			for (uint32_t j = 0; j < 8; ++j) {
+				const uint32_t v = lane_value(nu, 8u * j);
+				tmax = max(tmax, v);
+				tmin = v ? min(tmin, v) : tmin;
 			}
-			S.T = uni(tmax);
-			S.nmin = uni(tmin);
-			const uint32_t used = uni(min((uint32_t)__shfl(pre + avail, 63), rem));
+			S.T = tmax;
+			S.nmin = tmin;
+			const uint32_t used = min(lane_value(incl, 63), rem);
 			const uint32_t myvp = PECH_META_VP(my.meta);
 			uint32_t zp;
 			if (nu) {
@@ -660,19 +699,13 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 	u = adv_tab(lds, L_TAB4, u) ^ s2;
 	u = adv_tab(lds, L_TAB4, u) ^ s3;
 	u = adv_tab(lds, L_TAB4, u);
-	uint32_t o, lo, hi;
-	o = __shfl_xor(u, 1);
-	lo = (g8 & 1u) ? o : u;
-	hi = (g8 & 1u) ? u : o;
-	u = adv_tab(lds, L_TAB16, lo) ^ hi;
-	o = __shfl_xor(u, 2);
-	lo = (g8 & 2u) ? o : u;
-	hi = (g8 & 2u) ? u : o;
-	u = adv_tab(lds, L_TAB32, lo) ^ hi;
-	o = __shfl_xor(u, 4);
-	lo = (g8 & 4u) ? o : u;
-	hi = (g8 & 4u) ? u : o;
-	u = adv_tab(lds, L_TAB64, lo) ^ hi;
+	// Butterfly to the group's lane 0 only (the one that uses the result):
+	// at each stage the lower lane of a pair folds in its partner's value,
+	// read by a DPP row shift (lane i <- lane i + d, inside the 16-lane row
+	// that holds the whole group) instead of an LDS permute.
+	u = adv_tab(lds, L_TAB16, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x101, 0xf, 0xf, true);
+	u = adv_tab(lds, L_TAB32, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x102, 0xf, 0xf, true);
+	u = adv_tab(lds, L_TAB64, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x104, 0xf, 0xf, true);
 	uint32_t v = 0;
 	if (active && g8 == 0)
 		v = m ? shift_bytes(lds + L_POWB / 4u, m, u) : u;
@@ -680,9 +713,9 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 	// results in registers: one atomic per wave instead of 8 on one address.
 	const uint32_t o0 = uni(orig);
 	if (__ballot(active && orig != o0) == 0ull) {
-		v ^= __shfl_xor(v, 8);
-		v ^= __shfl_xor(v, 16);
-		v ^= __shfl_xor(v, 32);
+		// groups 0+1, 2+3, 4+5, 6+7 by a DPP row shift, then four lane reads
+		v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x108, 0xf, 0xf, true);
+		v = lane_value(v, 0) ^ lane_value(v, 16) ^ lane_value(v, 32) ^ lane_value(v, 48);
 		if ((threadIdx.x & 63u) == 0) {
 			// the workgroup's table: slot o0 % 64, claimed by CAS; a slot
 			// held by another buffer falls back to the global atomic
@@ -713,7 +746,7 @@ __device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, b
 template <bool COPY, uint32_t U>
 __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
 					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
-					  const uint32_t *__restrict__ nzs, uint32_t nchunks,
+					  const uint32_t *__restrict__ nzs, uint32_t n,
 					  const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min,
 					  const int64_t *__restrict__ deltas)
 {
@@ -723,6 +756,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
 	const uint32_t wave = uni(tid >> 6);
 	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
+	const uint32_t nchunks = (n + PECH_CHUNK - 1u) / PECH_CHUNK;
 
 	// Prologue (v0.11): three dependent global rounds before the first data
 	// instead of four, and no barrier until the ring is primed.  Every wave
@@ -731,8 +765,11 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	//   registers: issued first, their wait never drains the ring),
 	//   every chunk's row total and non-empty count (16 chunks per lane: the
 	//   wave scans them itself -- no workgroup scan, no barrier),
-	//   the row offsets of the chunk it most likely starts in (speculative:
-	//   exact for one chunk and for uniform batches; reloaded if wrong).
+	//   the row offsets of the chunk it most likely starts in, and the
+	//   descriptors of the 8 buffers at its likely start position
+	//   (speculative: exact for uniform batches; reloaded if wrong).
+	// Only the lanes whose entries exist load (every wave reads the same
+	// chunk totals: whole-array loads were 32 MiB of L2 reads per launch).
 	static_assert(1024u % PECH_MAIN_THREADS == 0u, "table fill: A_128 words split evenly over the threads");
 	static_assert(PECH_MAX_CHUNKS == 64u * 16u, "wave scan: 16 chunks per lane");
 	static_assert(PECH_CHUNK == 64u * 16u, "find: 16 row offsets per lane");
@@ -748,18 +785,35 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 	for (uint32_t k = 0; k < TPT; ++k)
 		tv[k] = c4[min(tid + k * PECH_MAIN_THREADS, NT4 - 1u)];
-	// (partials / nzs hold PECH_MAX_CHUNKS entries: whole-array loads are in bounds)
+	// (partials / nzs hold PECH_MAX_CHUNKS entries, lrs whole chunks)
 	u32x4 pv4[4], nv4[4], lr4[4];
 #pragma unroll
-	for (uint32_t k = 0; k < 4; ++k) {
-		pv4[k] = ((const u32x4 *)partials)[lane * 4u + k];
-		nv4[k] = ((const u32x4 *)nzs)[lane * 4u + k];
+	for (uint32_t k = 0; k < 4; ++k) // defined values where nothing loads (a select of undef may fold)
+		pv4[k] = nv4[k] = lr4[k] = (u32x4)(0u);
+	if (lane * 16u < nchunks) {
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			pv4[k] = ((const u32x4 *)partials)[lane * 4u + k];
+			nv4[k] = ((const u32x4 *)nzs)[lane * 4u + k];
+		}
 	}
 	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
-	const uint32_t cg = uni((uint32_t)((uint64_t)wglob * nchunks / W)); // likely start chunk
+	// likely start position: exact for uniform batches (a double quotient of
+	// integers is exact when it is one; a near miss only costs a reload)
+	const uint32_t pg = uni(min((uint32_t)((double)wglob * (double)n / (double)W), n - 1u));
+	const uint32_t cg = pg >> 10;                                   // and chunk
+	if (lane * 16u < n - cg * PECH_CHUNK) {
 #pragma unroll
-	for (uint32_t k = 0; k < 4; ++k)
-		lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + lane * 16u))[k];
+		for (uint32_t k = 0; k < 4; ++k)
+			lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + lane * 16u))[k];
+	}
+	pech_core spec; // cores[pg + grp] (pg + 7 may run into lrs: workspace memory, used only if in the chunk)
+	{
+		const u32x4 v = ((const u32x4 *)cores)[pg + grp];
+		spec.vbase = ((uint64_t)v.y << 32) | v.x;
+		spec.rows = v.z;
+		spec.meta = v.w;
+	}
 
 	// the wave's own exclusive scan of the chunk totals
 	uint32_t pc[16], nc[16], lsum = 0;
@@ -770,17 +824,11 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		nc[k] = real ? nv4[k >> 2][k & 3u] : 0u;
 		lsum += pc[k];
 	}
-	uint32_t incl = lsum;
-#pragma unroll
-	for (uint32_t d = 1; d < 64; d <<= 1) {
-		const uint32_t y = __shfl_up(incl, d);
-		if (lane >= d)
-			incl += y;
-	}
-	const uint32_t Rtot = uni(__shfl(incl, 63));
+	const uint32_t incl = wave_incl_scan(lsum);
+	const uint32_t Rtot = lane_value(incl, 63);
 	STAMP(t_scan);
 	// Every wave gets an equal share of the batch's rows (at least rpw_min).
-	const uint32_t rpw_eq = (uint32_t)(((uint64_t)Rtot + W - 1u) / W);
+	const uint32_t rpw_eq = Rtot ? (Rtot - 1u) / W + 1u : 0u;
 	const uint32_t rpw = max(rpw_min, rpw_eq);
 	const uint64_t wg0 = (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
 	if (wg0 >= Rtot)
@@ -814,15 +862,13 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			nzj = le ? nc[k] : nzj;
 			pre += pc[k];
 		}
-		uint32_t jc = cnt;
-#pragma unroll
-		for (uint32_t d = 1; d < 64; d <<= 1)
-			jc += __shfl_xor(jc, d);
-		const uint32_t j = uni(jc) - 1u;
-		pj = uni(__shfl(pj, j >> 4));
-		nzj = uni(__shfl(nzj, j >> 4));
+		// (prefixes are nondecreasing: the lanes with cnt > 0 are a prefix)
+		const uint32_t Lj = last_lane_with(cnt);
+		const uint32_t j = Lj * 16u + lane_value(cnt, Lj) - 1u;
+		pj = lane_value(pj, Lj);
+		nzj = lane_value(nzj, Lj);
 		const uint32_t rr = r0 - pj;
-		if (j != cg) { // speculation missed: the start chunk's row offsets now
+		if (j != cg && lane * 16u < nzj) { // speculation missed: the start chunk's row offsets now
 #pragma unroll
 			for (uint32_t k = 0; k < 4; ++k)
 				lr4[k] = ((const u32x4 *)(lrs + j * PECH_CHUNK + lane * 16u))[k];
@@ -837,21 +883,20 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			c2 += ok ? 1u : 0u;
 			lo = ok ? max(lo, e) : lo;
 		}
-#pragma unroll
-		for (uint32_t d = 1; d < 64; d <<= 1) {
-			c2 += __shfl_xor(c2, d);
-			lo = max(lo, (uint32_t)__shfl_xor(lo, d));
-		}
-		p0 = uni(j * PECH_CHUNK + c2 - 1u);
-		lr0 = uni(rr - lo);
+		// (offsets increase over the non-empty cores: the lanes with c2 > 0
+		// are a prefix, and the last of them holds the largest offset <= rr)
+		const uint32_t Lp = last_lane_with(c2);
+		const uint32_t cpos = Lp * 16u + lane_value(c2, Lp);
+		p0 = j * PECH_CHUNK + cpos - 1u;
+		lr0 = rr - lane_value(lo, Lp);
 #ifdef PECH_DEBUG_BOUNDS
-		if (lane == 0 && (j >= nchunks || c2 == 0 || c2 > nzj || lr0 >= cores[p0].rows))
-			printf("PECH OOB prologue blk %u wave %u r0 %u j %u cg %u nchunks %u nzj %u c2 %u rr %u lo %u rows %u\n",
-			       blockIdx.x, wave, r0, j, cg, nchunks, nzj, c2, rr, lo, cores[min(p0, nchunks * PECH_CHUNK - 1u)].rows);
+		if (lane == 0 && (j >= nchunks || cpos == 0 || cpos > nzj || lr0 >= cores[p0].rows))
+			printf("PECH OOB prologue blk %u wave %u r0 %u j %u cg %u nchunks %u nzj %u cpos %u rr %u rows %u\n",
+			       blockIdx.x, wave, r0, j, cg, nchunks, nzj, cpos, rr, cores[min(p0, nchunks * PECH_CHUNK - 1u)].rows);
 #endif
 	}
 	STAMP(t_find);
-	Step S = plan_step<COPY>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp);
+	Step S = plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, spec, pg);
 	STAMP(t_plan);
 	if (S.T)
 		RING_PRIME(S, ring);
@@ -964,7 +1009,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		__threadfence_block(); // table updates before the count (compiler and LDS order)
 		if (lane == 0)
 			done = atomicAdd(lds + L_DEFER_DONE / 4u, 1u);
-		done = uni(__shfl(done, 0));
+		done = lane_value(done, 0);
 		__threadfence_block();
 		static_assert(PECH_DEFER_SLOTS == 64u, "one slot per lane of the flushing wave");
 		if (done == PECH_MAIN_WAVES - 1u) {
@@ -1003,22 +1048,22 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 
 extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_main(
 	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
-	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	const uint32_t *__restrict__ nzs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
 	uint32_t rpw_min)
 {
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
-	main_body<false, PECH_U>(lds, cores, lrs, partials, nzs, nchunks, consts, out, rpw_min, nullptr);
+	main_body<false, PECH_U>(lds, cores, lrs, partials, nzs, n, consts, out, rpw_min, nullptr);
 }
 
 // fused CRC + copy (include/pech_crc32c.h crc32c_dev_copy_batch_*): the same
 // walk, every consumed 16-byte piece also stored to its destination
 extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_main_copy(
 	const pech_core *__restrict__ cores, const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
-	const uint32_t *__restrict__ nzs, uint32_t nchunks, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	const uint32_t *__restrict__ nzs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
 	uint32_t rpw_min, const int64_t *__restrict__ deltas)
 {
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
-	main_body<true, PECH_U_COPY>(lds, cores, lrs, partials, nzs, nchunks, consts, out, rpw_min, deltas);
+	main_body<true, PECH_U_COPY>(lds, cores, lrs, partials, nzs, n, consts, out, rpw_min, deltas);
 }
 
 // ---- host-side launchers (used by crc32c_api.cpp) -------------------------
@@ -1053,16 +1098,15 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 				       uint32_t ncu, uint32_t rpw_min, int copy, hipStream_t stream, hipEvent_t ev_start,
 				       hipEvent_t ev_stop)
 {
-	const uint32_t nch = (n + PECH_CHUNK - 1) / PECH_CHUNK;
 	if (copy)
 		hipExtLaunchKernelGGL(pech_crc32c_main_copy, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop,
 				      0u, (const pech_core *)ws->cores, (const uint32_t *)ws->lrs,
-				      (const uint32_t *)ws->partials, (const uint32_t *)ws->nzs, nch, consts, out, rpw_min,
+				      (const uint32_t *)ws->partials, (const uint32_t *)ws->nzs, n, consts, out, rpw_min,
 				      (const int64_t *)ws->deltas);
 	else
 		hipExtLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop,
 				      0u, (const pech_core *)ws->cores, (const uint32_t *)ws->lrs,
-				      (const uint32_t *)ws->partials, (const uint32_t *)ws->nzs, nch, consts, out, rpw_min);
+				      (const uint32_t *)ws->partials, (const uint32_t *)ws->nzs, n, consts, out, rpw_min);
 	return hipGetLastError();
 }
 
@@ -1070,6 +1114,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.11 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.12 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }
