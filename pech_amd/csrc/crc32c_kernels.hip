@@ -802,17 +802,24 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// integers is exact when it is one; a near miss only costs a reload)
 	const uint32_t pg = uni(min((uint32_t)((double)wglob * (double)n / (double)W), n - 1u));
 	const uint32_t cg = pg >> 10;                                   // and chunk
-	if (lane * 16u < n - cg * PECH_CHUNK) {
-#pragma unroll
-		for (uint32_t k = 0; k < 4; ++k)
-			lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + lane * 16u))[k];
-	}
+	const uint32_t lrg = lrs[pg]; // pg's row offset in its chunk
 	pech_core spec; // cores[pg + grp] (pg + 7 may run into lrs: workspace memory, used only if in the chunk)
 	{
 		const u32x4 v = ((const u32x4 *)cores)[pg + grp];
 		spec.vbase = ((uint64_t)v.y << 32) | v.x;
 		spec.rows = v.z;
 		spec.meta = v.w;
+	}
+
+	// last: the speculative row offsets (vmcnt is in order, so the exact
+	// check below waits for the loads above only).  Unconditional -- a load
+	// under a branch gets a vmcnt(0) at the join -- with lanes past the
+	// chunk's buffers reading lane 0's lines (no extra traffic; masked later).
+	{
+		const uint32_t ll = lane * 16u < n - cg * PECH_CHUNK ? lane : 0u;
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k)
+			lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + ll * 16u))[k];
 	}
 
 	// the wave's own exclusive scan of the chunk totals
@@ -850,7 +857,28 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			u32x4{nc[4 * k], nc[4 * k + 1], nc[4 * k + 2], nc[4 * k + 3]}; // braces: a parenthesised list is a comma splat
 
 	uint32_t p0 = 0, lr0 = 0;
+	bool found = false;
 	if (rem_all) {
+		// The speculated position first, checked exactly: buffer pg holds
+		// row r0 iff its global offset (chunk prefix + lrs[pg]) <= r0 <
+		// offset + its rows.  Uniform batches start here without waiting for
+		// the row-offset scan below.
+		const uint32_t lc = cg >> 4, kc = cg & 15u;
+		uint32_t prec = incl - lsum, nzc = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 16; ++k) {
+			prec += k < kc ? pc[k] : 0u;
+			nzc = k == kc ? nc[k] : nzc;
+		}
+		const uint32_t og = lane_value(prec, lc) + uni(lrg);
+		const uint32_t rg = uni(spec.rows); // lane 0: cores[pg]
+		if (cg < nchunks && (pg & 1023u) < lane_value(nzc, lc) && og <= r0 && r0 - og < rg) {
+			p0 = pg;
+			lr0 = r0 - og;
+			found = true;
+		}
+	}
+	if (rem_all && !found) {
 		// start chunk j: the last chunk whose prefix is <= r0 (non-empty,
 		// since r0 < Rtot); its prefix and non-empty count
 		uint32_t pre = incl - lsum, cnt = 0, pj = 0, nzj = 0;
