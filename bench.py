@@ -318,6 +318,8 @@ def main():
         probe = stream_probe("copy" if dsts else "read", max(1, batch_bytes >> 20))
         if probe:
             line["roofline"]["probe"] = dict(probe, frac_of_probe=round(achieved_gbs / probe["GBps"], 4))
+            if "best_shape" in probe:
+                line["roofline"]["probe"]["best_shape"]["frac"] = round(achieved_gbs / probe["best_shape"]["GBps"], 4)
 
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -514,9 +516,18 @@ def stream_probe(kind, mib):
         return None
     res = json.loads(r.stdout.decode())["results"][0]
     gbs = res.get("GBps_read_plus_write", res.get("GBps"))
-    return {"kind": kind, "GBps": gbs, "us_per_launch": res["us"],
-            "what": f"tools/sched_probe.hip: same access shape, nontemporal, static shares, {mib} MiB" +
-                    (f" read + {mib} MiB written" if kind == "copy" else " read") + " per launch"}
+    out = {"kind": kind, "GBps": gbs, "us_per_launch": res["us"],
+           "what": f"tools/sched_probe.hip: same access shape, nontemporal, static shares, {mib} MiB" +
+                   (f" read + {mib} MiB written" if kind == "copy" else " read") + " per launch"}
+    # The fastest shape measured for the same bytes (a non-persistent grid,
+    # one 16-byte nontemporal element per thread): a stricter denominator
+    # that no table-driven persistent kernel reaches (profiles/r02/shape_probes.txt).
+    r = subprocess.run([exe, "10", "grid", str(mib)], capture_output=True, timeout=120)
+    if r.returncode == 0:
+        res = json.loads(r.stdout.decode())["results"][1 if kind == "copy" else 0]
+        out["best_shape"] = {"GBps": res["GBps"], "us_per_launch": res["us"], "what": res["probe"] +
+                             ": non-persistent grid, one 16-byte element per thread"}
+    return out
 
 
 def shard_parity(shards, offs, sizes, rotate, P):

@@ -479,6 +479,133 @@ __global__ __launch_bounds__(1024, 1) void k_copy(const uint8_t *p, uint8_t *q, 
 	}
 }
 
+// read+write copy, static shares, but each wave-instruction covers 1 KiB of
+// consecutive rows (lane l: row 8k + l/8, piece l%8) instead of 8 rows of 8
+// separate streams
+template <bool NT>
+__global__ __launch_bounds__(1024, 1) void k_copy_wide(const uint8_t *p, uint8_t *q, uint32_t R)
+{
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const uint64_t lo = (uint64_t)r0 * ROW + 16u * lane, hi = (uint64_t)r1 * ROW;
+	u32x4 ring[D];
+	for (uint64_t a = lo; a < hi; a += D * 1024u) {
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			const uint64_t ai = min(a + i * 1024u, hi - 16u);
+			ring[i] = NT ? __builtin_nontemporal_load((g_u32x4 *)(p + ai)) : *(g_u32x4 *)(p + ai);
+		}
+#pragma unroll
+		for (int i = 0; i < D; ++i)
+			if (a + i * 1024u < hi) {
+				if (NT)
+					__builtin_nontemporal_store(ring[i], (g_u32x4w *)(q + a + i * 1024u));
+				else
+					*(g_u32x4w *)(q + a + i * 1024u) = ring[i];
+			}
+	}
+}
+
+// plain one-element-per-thread float4 copy over a large grid (not persistent)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copy_grid(const uint8_t *p, uint8_t *q, uint64_t n16)
+{
+	const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+	if (i < n16) {
+		const u32x4 v = NT ? __builtin_nontemporal_load((g_u32x4 *)(p + 16u * i)) : *(g_u32x4 *)(p + 16u * i);
+		if (NT)
+			__builtin_nontemporal_store(v, (g_u32x4w *)(q + 16u * i));
+		else
+			*(g_u32x4w *)(q + 16u * i) = v;
+	}
+}
+
+// plain one-element-per-thread read over a large grid (not persistent)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_read_grid(const uint8_t *p, uint64_t n16, uint32_t *out)
+{
+	const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+	if (i < n16) {
+		const u32x4 v = NT ? __builtin_nontemporal_load((g_u32x4 *)(p + 16u * i)) : *(g_u32x4 *)(p + 16u * i);
+		if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u)
+			out[i & 1023u] = 1u;
+	}
+}
+
+// persistent waves over interleaved tiles: wave w takes tiles w, w + W, ...
+// of TR rows; in a tile its 8 groups each walk TR/8 consecutive rows (the
+// CRC kernel's group shape), D rows in flight.  All waves stay inside a
+// window of about W tiles, moving through memory together (DRAM locality),
+// instead of 32K streams spread over the whole batch.
+template <bool COPY, uint32_t TR>
+__global__ __launch_bounds__(1024, 1) void k_tiles(const uint8_t *p, uint8_t *q, uint32_t R, uint32_t *out)
+{
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	constexpr uint32_t PER = TR / 8u;
+	static_assert(PER % D == 0, "tile slice: whole ring blocks");
+	u32x4 acc = (u32x4)(0u), ring[D];
+	for (uint32_t t = w; (uint64_t)t * TR < R; t += W) {
+		const uint32_t row0 = t * TR + grp * PER;
+		for (uint32_t r = 0; r < PER; r += D) {
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				ring[i] = ld(p, min(row0 + r + i, R - 1u), g8);
+#pragma unroll
+			for (int i = 0; i < D; ++i) {
+				if (COPY) {
+					if (row0 + r + i < R)
+						__builtin_nontemporal_store(ring[i], (g_u32x4w *)(q + (uint64_t)(row0 + r + i) * ROW + 16u * g8));
+				} else {
+					acc ^= ring[i];
+				}
+			}
+		}
+	}
+	if (!COPY && (acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u)
+		out[w] = 1u;
+}
+
+// copy variants for the occupancy question: the static copy with DD rows in
+// flight and MINB workgroups per CU (MINB 2: 32 waves per CU, <= 64 VGPRs)
+template <int DD, int MINB>
+__global__ __launch_bounds__(1024, MINB) void k_copy_occ(const uint8_t *p, uint8_t *q, uint32_t R)
+{
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const PStep s = make_step(r0, r1 - r0, grp);
+	u32x4 ring[DD];
+	for (uint32_t r = 0; r < s.n; r += DD) {
+#pragma unroll
+		for (int i = 0; i < DD; ++i)
+			ring[i] = ld(p, s.row + min(r + i, s.n - 1u), g8);
+#pragma unroll
+		for (int i = 0; i < DD; ++i)
+			if (r + i < s.n)
+				__builtin_nontemporal_store(ring[i], (g_u32x4w *)(q + (uint64_t)(s.row + r + i) * ROW + 16u * g8));
+	}
+}
+
+// grid copy, K float4 per thread (grid-stride inside the workgroup's block)
+template <int K>
+__global__ __launch_bounds__(256) void k_copy_gridk(const uint8_t *p, uint8_t *q, uint64_t n16)
+{
+	const uint64_t b = blockIdx.x * 256ull * K + threadIdx.x;
+	u32x4 v[K];
+#pragma unroll
+	for (int k = 0; k < K; ++k)
+		v[k] = __builtin_nontemporal_load((g_u32x4 *)(p + 16u * min(b + 256u * k, n16 - 1u)));
+#pragma unroll
+	for (int k = 0; k < K; ++k)
+		if (b + 256u * k < n16)
+			__builtin_nontemporal_store(v[k], (g_u32x4w *)(q + 16u * (b + 256u * k)));
+}
+
 static int g_entries;
 static const char *sep(void)
 {
@@ -721,6 +848,118 @@ int main(int argc, char **argv)
 		}
 		printf("%s  {\"probe\": \"copy static (read+write)\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}",
 		       sep(), tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		const char *names[4] = {"copy wide 1 KiB/wave nt", "copy wide 1 KiB/wave", "copy grid float4 nt", "copy grid float4"};
+		for (int v = 0; v < 4; ++v) {
+			tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				if (v == 0)
+					hipLaunchKernelGGL(k_copy_wide<true>, dim3(ncu), dim3(1024), 0, 0, src, buf[2], R);
+				else if (v == 1)
+					hipLaunchKernelGGL(k_copy_wide<false>, dim3(ncu), dim3(1024), 0, 0, src, buf[2], R);
+				else if (v == 2)
+					hipLaunchKernelGGL(k_copy_grid<true>, dim3((unsigned)(bytes / 16 / 256)), dim3(256), 0, 0, src, buf[2],
+							   (uint64_t)(bytes / 16));
+				else
+					hipLaunchKernelGGL(k_copy_grid<false>, dim3((unsigned)(bytes / 16 / 256)), dim3(256), 0, 0, src, buf[2],
+							   (uint64_t)(bytes / 16));
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v],
+			       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (all || !strcmp(which, "locality")) {
+		const char *names[] = {"read grid float4 nt", "read tiles 8 KiB", "read tiles 32 KiB", "read tiles 128 KiB",
+				       "copy tiles 8 KiB", "copy tiles 32 KiB", "copy tiles 128 KiB"};
+		for (int v = 0; v < 7; ++v) {
+			float tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				switch (v) {
+				case 0:
+					hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(bytes / 16 / 256)), dim3(256), 0, 0, src,
+							   (uint64_t)(bytes / 16), out);
+					break;
+				case 1: hipLaunchKernelGGL((k_tiles<false, 64>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 2: hipLaunchKernelGGL((k_tiles<false, 256>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 3: hipLaunchKernelGGL((k_tiles<false, 1024>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 4: hipLaunchKernelGGL((k_tiles<true, 64>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 5: hipLaunchKernelGGL((k_tiles<true, 256>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				default: hipLaunchKernelGGL((k_tiles<true, 1024>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				}
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			const double f = v >= 4 ? 2.0 : 1.0;
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps%s\": %.1f}", sep(), names[v], tot / reps * 1e3,
+			       v >= 4 ? "_read_plus_write" : "", f * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (!strcmp(which, "grid")) { // the best shapes measured: one float4 per thread, non-persistent grid, nt
+		for (int v = 0; v < 2; ++v) {
+			float tot = 0;
+			const uint64_t n16 = bytes / 16;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				if (v == 0)
+					hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, n16, out);
+				else
+					hipLaunchKernelGGL(k_copy_grid<true>, dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, buf[2], n16);
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}", sep(),
+			       v ? "copy grid float4 nt (read+write)" : "read grid float4 nt", tot / reps * 1e3,
+			       (v ? 2.0 : 1.0) * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (all || !strcmp(which, "copyocc")) {
+		const char *names[] = {"copy static D8 16 waves/CU", "copy static D4 16 waves/CU", "copy static D16 16 waves/CU",
+				       "copy static D8 32 waves/CU", "copy static D4 32 waves/CU", "copy grid 1 float4/thread",
+				       "copy grid 4 float4/thread", "copy grid 16 float4/thread"};
+		for (int v = 0; v < 8; ++v) {
+			float tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				const uint64_t n16 = bytes / 16;
+				switch (v) {
+				case 0: hipLaunchKernelGGL((k_copy_occ<8, 1>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 1: hipLaunchKernelGGL((k_copy_occ<4, 1>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 2: hipLaunchKernelGGL((k_copy_occ<16, 1>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 3: hipLaunchKernelGGL((k_copy_occ<8, 2>), dim3(2 * ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 4: hipLaunchKernelGGL((k_copy_occ<4, 2>), dim3(2 * ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 5: hipLaunchKernelGGL((k_copy_gridk<1>), dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, buf[2], n16); break;
+				case 6: hipLaunchKernelGGL((k_copy_gridk<4>), dim3((unsigned)(n16 / 1024)), dim3(256), 0, 0, src, buf[2], n16); break;
+				default: hipLaunchKernelGGL((k_copy_gridk<16>), dim3((unsigned)(n16 / 4096)), dim3(256), 0, 0, src, buf[2], n16); break;
+				}
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v],
+			       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
 	}
 	printf("\n]}\n");
 	return 0;
