@@ -172,6 +172,48 @@ def test_c4_mixed_sizes_parity(torch_dev, P):
     assert np.array_equal(got, O.crcs(buf.cpu().numpy(), offs, sizes))
 
 
+@pytest.mark.parametrize("case", ["uniform-odd-n", "uniform-unaligned", "uniform-with-holes", "empty-first-chunk",
+                                  "many-chunks", "fewer-buffers-than-waves"])
+def test_prologue_start_search(torch_dev, P, case):
+    """The main kernel's prologue speculates each wave's start position and
+    checks it exactly (uniform batches start there; others fall back to the
+    row-offset scan).  Batches around that check: uniform sizes at batch
+    sizes that are no multiple of a chunk, unaligned buffers (virtual
+    leading pieces), uniform batches with tiny/empty buffers sprinkled in
+    (compacted positions shift the guess), a first chunk with no core rows at
+    all, more than 16 chunks (the chunk scan spans lanes), and fewer
+    buffers than waves."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(sum(map(ord, case)))
+    gap = 0
+    if case == "uniform-odd-n":
+        sizes = [12288] * 5001
+    elif case == "uniform-unaligned":
+        sizes, gap = [4096 + 7] * 3001, 9
+    elif case == "uniform-with-holes":
+        sizes = [8192] * 6000
+        for i in rng.choice(6000, 300, replace=False):
+            sizes[i] = int(rng.integers(0, 31))
+    elif case == "empty-first-chunk":
+        sizes = [int(x) for x in rng.integers(0, 16, 1024)] + [65536] * 1500
+    elif case == "many-chunks":
+        sizes = [2048] * 40000 + [int(x) for x in rng.integers(0, 100000, 500)]
+    else:
+        sizes = [1 << 20] * 37 + [333333] * 5
+    n = len(sizes)
+    offs = np.zeros(n, dtype=np.int64)
+    pos = 3
+    for i, L in enumerate(sizes):
+        offs[i] = pos
+        pos += L + gap
+    buf = torch.randint(0, 256, (pos + 64,), dtype=torch.uint8, device=dev)
+    seeds = [int(x) for x in rng.integers(0, 1 << 32, n)] if case in ("uniform-odd-n", "many-chunks") else None
+    got = dev_crcs(torch, P, buf, offs, sizes, seeds)
+    host = buf.cpu().numpy()
+    want = O.crcs(host, offs, sizes, seeds)
+    assert np.array_equal(got, want), int(np.sum(got != want))
+
+
 def test_single_huge_buffer_split_over_all_groups(torch_dev, P):
     torch, dev = torch_dev
     L = (96 << 20) + 12345
