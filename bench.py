@@ -83,6 +83,8 @@ def parse():
                          "pass that gives `value`; a one-stream pass always gives the per-launch roofline")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
+    ap.add_argument("--data", choices=["random", "zeros", "ones"], default="random",
+                    help="payload bytes: uniform random (default) or the constant sensitivity rows of SURVEY 8(d)")
     ap.add_argument("--profile-json", default=None, help="PMC summary (profiles/*.json) to fill roofline.traffic")
     ap.add_argument("--rotate", type=int, default=None,
                     help="distinct resident batches to rotate over (default per config; a multiple of --streams)")
@@ -156,7 +158,11 @@ def main():
                 gen.manual_seed(seed)
                 self.bufs, self.descs = [], []
                 for r in range(rotate):
-                    b = torch.randint(0, 256, (batch_bytes,), dtype=torch.uint8, device=self.dev, generator=gen)
+                    if args.data == "random":
+                        b = torch.randint(0, 256, (batch_bytes,), dtype=torch.uint8, device=self.dev, generator=gen)
+                    else:  # SURVEY 8(d) sensitivity rows: constant bytes (every lane looks up the same entries)
+                        b = torch.full((batch_bytes,), 0 if args.data == "zeros" else 0xFF, dtype=torch.uint8,
+                                       device=self.dev)
                     self.bufs.append(b)
                     self.descs.append(P.make_descs(b.data_ptr() + offs, sizes, device=self.dev))
                 self.outs = [torch.zeros(n, dtype=torch.int32, device=self.dev) for _ in range(rotate)]
@@ -276,7 +282,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (uniform random bytes, torch.randint on device), seed 0 per buffer",
+        "data": ("synthetic (uniform random bytes, torch.randint on device), seed 0 per buffer" if args.data == "random"
+                 else f"synthetic constant bytes ({'0x00' if args.data == 'zeros' else '0xFF'}), seed 0 per buffer"),
         "config": {"workload": desc + ("; fused CRC + copy to a second buffer (read + write)" if dsts else ""),
                    "buffers_per_gpu": n, "bytes_per_gpu_per_step": batch_bytes,
                    "parallelism": (f"single-thread: one process drives {len(shards)} shard(s) on device(s) "
