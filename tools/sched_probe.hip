@@ -606,6 +606,58 @@ __global__ __launch_bounds__(256) void k_copy_gridk(const uint8_t *p, uint8_t *q
 			__builtin_nontemporal_store(v[k], (g_u32x4w *)(q + 16u * (b + 256u * k)));
 }
 
+// Static shares for the first ncu workgroups over rows [0, Rs), then X
+// extra workgroups over [Rs, R) in equal pieces: the dispatcher hands each
+// extra workgroup to the first CU whose static workgroup has exited (one
+// workgroup per CU at 1024 threads + the kernel's LDS), balancing the end of
+// the launch with no atomics.  Extra workgroups idle `idle` us first (the CRC
+// kernel's prologue).  Same read loop for both kinds.
+__global__ __launch_bounds__(1024, 1) void k_extra(const uint8_t *p, uint32_t R, uint32_t ncu, uint32_t Rs, uint32_t X,
+						   uint32_t idle, uint32_t *out)
+{
+	__shared__ uint32_t pad[36 * 1024]; // 144 KiB: one workgroup per CU, as the CRC kernel
+	const uint32_t b = blockIdx.x, wave = threadIdx.x / 64u;
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	uint64_t lo, hi;
+	uint32_t wi, nw;
+	if (b < ncu) {
+		lo = 0;
+		hi = Rs;
+		wi = b * WAVES + wave;
+		nw = ncu * WAVES;
+	} else {
+		const uint64_t k = b - ncu;
+		lo = Rs + (uint64_t)(R - Rs) * k / X;
+		hi = Rs + (uint64_t)(R - Rs) * (k + 1) / X;
+		wi = wave;
+		nw = WAVES;
+		const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+		while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * idle)
+			__builtin_amdgcn_s_sleep(8);
+	}
+	const uint32_t r0 = (uint32_t)(lo + (hi - lo) * wi / nw), r1 = (uint32_t)(lo + (hi - lo) * (wi + 1) / nw);
+	const PStep s = make_step(r0, r1 - r0, grp);
+	u32x4 acc = (u32x4)(0u), ring[D];
+	if (s.T) {
+#pragma unroll
+		for (int i = 0; i + 1 < D; ++i)
+			ring[i] = ld(p, s.row + min((uint32_t)i, s.n - 1u), g8);
+		for (uint32_t r = 0; r < s.T; r += D) {
+#pragma unroll
+			for (int i = 0; i < D; ++i) {
+				ring[(i + D - 1) % D] = ld(p, s.row + min(r + i + D - 1, s.n - 1u), g8);
+				if (r + i < s.n)
+					acc ^= ring[i];
+			}
+		}
+	}
+	pad[threadIdx.x] = acc.x;
+	__syncthreads();
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w ^ pad[(threadIdx.x + 1u) & 1023u];
+	if (x == 0x12345678u)
+		out[b] = x;
+}
+
 static int g_entries;
 static const char *sep(void)
 {
@@ -905,6 +957,29 @@ int main(int argc, char **argv)
 			const double f = v >= 4 ? 2.0 : 1.0;
 			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps%s\": %.1f}", sep(), names[v], tot / reps * 1e3,
 			       v >= 4 ? "_read_plus_write" : "", f * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (!strcmp(which, "extra")) {
+		struct {
+			uint32_t permille, X, idle;
+		} ex[] = {{0, 0, 0}, {50, 256, 0}, {100, 256, 0}, {100, 512, 0}, {200, 512, 0}, {100, 256, 4},
+			  {100, 512, 4}, {200, 512, 4}, {200, 1024, 4}, {0, 0, 0}};
+		for (size_t v = 0; v < sizeof(ex) / sizeof(ex[0]); ++v) {
+			float tot = 0;
+			const uint32_t Rs = (uint32_t)((uint64_t)R * (1000u - ex[v].permille) / 1000u);
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				hipLaunchKernelGGL(k_extra, dim3(ncu + ex[v].X), dim3(1024), 0, 0, buf[(r + 4) % 2], R, (uint32_t)ncu, Rs,
+						   ex[v].X, ex[v].idle, out);
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			printf("%s  {\"probe\": \"static + %u extra WGs over the last %.1f%% (idle %u us)\", \"us\": %.2f, \"GBps\": %.1f}",
+			       sep(), ex[v].X, ex[v].permille / 10.0, ex[v].idle, tot / reps * 1e3, bytes / (tot / reps * 1e-3) / 1e9);
 		}
 	}
 	if (!strcmp(which, "grid")) { // the best shapes measured: one float4 per thread, non-persistent grid, nt
