@@ -85,6 +85,13 @@ static void build_consts(uint32_t *c)
 	// A_1: the reference byte table (include/crc32c.h:16-81), regenerated
 	for (uint32_t e = 0; e < 256; ++e)
 		c[PECH_C_TAB1 + e] = gf2_mulmod(CRC32C_X8, e);
+	// XINV[k] = x^(-8k): undoes k trailing zero bytes (a core's last line)
+	const uint32_t xinv8 = gf2_xinv8n(1);
+	uint32_t acc = CRC32C_ONE;
+	for (uint32_t k = 0; k < 128; ++k) {
+		c[PECH_C_XINV + k] = acc;
+		acc = gf2_mulmod(acc, xinv8);
+	}
 }
 
 // ---------------------------------------------------------------------------

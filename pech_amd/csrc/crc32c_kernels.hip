@@ -67,7 +67,8 @@
 #define L_NZ (L_POWB + 1536u)    // 4 KiB: chunk non-empty counts
 #define L_DEFER (L_NZ + 4096u)   // 512 B: split-step results, keyed by output slot
 #define L_DEFER_DONE (L_DEFER + 8u * PECH_DEFER_SLOTS) // waves of the workgroup done
-#define L_BYTES (L_DEFER_DONE + 16u)
+#define L_XINV (L_DEFER_DONE + 16u) // 512 B: x^(-8k), k < 128
+#define L_BYTES (L_XINV + 512u)
 static_assert(L_BYTES <= 160u * 1024u, "main kernel LDS over 160 KiB");
 
 static_assert(L_POWB - L_TAB4 == 4u * (PECH_C_POWB - PECH_C_TAB4), "LDS/consts layout mismatch");
@@ -183,23 +184,32 @@ __device__ __forceinline__ uint32_t shift_bytes(const uint32_t *powb, uint64_t m
 }
 
 // ---- plan kernel ----------------------------------------------------------
-// byte-wise reference update (include/crc32c.h:92-93) on the LDS table
-__device__ __forceinline__ uint32_t crc_bytes(const uint32_t *t1, uint32_t crc, uint64_t addr, uint32_t n)
+// byte-wise reference update (include/crc32c.h:92-93) on the LDS table, over
+// bytes [lo, hi) of a 16-byte block held in registers (0 <= lo <= hi <= 16)
+__device__ __forceinline__ uint32_t crc_block(const uint32_t *t1, uint32_t crc, u32x4 v, uint32_t lo, uint32_t hi)
 {
-	const g_u8 *q = (const g_u8 *)addr;
-	for (uint32_t i = 0; i < n; ++i)
-		crc = t1[(crc ^ q[i]) & 0xFFu] ^ (crc >> 8);
+#pragma unroll
+	for (uint32_t k = 0; k < 16; ++k) {
+		const uint32_t w = k < 4 ? v.x : (k < 8 ? v.y : (k < 12 ? v.z : v.w));
+		const uint32_t byte = (w >> (8u * (k & 3u))) & 0xFFu;
+		if (k >= lo && k < hi)
+			crc = t1[(crc ^ byte) & 0xFFu] ^ (crc >> 8);
+	}
 	return crc;
 }
 
-// byte copy of [src, src + n) to src + dl (fused-copy variant: heads, tails
-// and buffers without a full aligned piece)
-__device__ __forceinline__ void copy_bytes(uint64_t src, int64_t dl, uint32_t n)
+// fused-copy variant: bytes [lo, hi) of the block whose first byte is at
+// `dst` in the destination (heads, tails and buffers without a full aligned
+// piece; the main kernel stores the rest)
+__device__ __forceinline__ void copy_block(u32x4 v, uint32_t lo, uint32_t hi, uint64_t dst)
 {
-	const g_u8 *q = (const g_u8 *)src;
-	__attribute__((address_space(1))) uint8_t *d = (__attribute__((address_space(1))) uint8_t *)(src + dl);
-	for (uint32_t i = 0; i < n; ++i)
-		d[i] = q[i];
+	__attribute__((address_space(1))) uint8_t *d = (__attribute__((address_space(1))) uint8_t *)dst;
+#pragma unroll
+	for (uint32_t k = 0; k < 16; ++k) {
+		const uint32_t w = k < 4 ? v.x : (k < 8 ? v.y : (k < 12 ? v.z : v.w));
+		if (k >= lo && k < hi)
+			d[k] = (uint8_t)(w >> (8u * (k & 3u)));
+	}
 }
 
 // COPY: also dst[b] <- bytes of buffer b (fused CRC + copy); the plan kernel
@@ -227,6 +237,22 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	const uint32_t tvp = consts[PECH_C_POWB + min(tid, 383u)];
 	if (b >= n)
 		d.len = 0;
+	// The bytes outside the main kernel's rows (head, tail, or a whole buffer
+	// without a full aligned piece) lie in the aligned 16-byte blocks holding
+	// the buffer's first and last bytes: two vector loads in flight together
+	// (a byte loop here cost one global round trip per byte).  An aligned
+	// 16-byte block never crosses a page, so it is readable whenever one of
+	// its bytes is.  A block with nothing to read (an aligned start or end,
+	// an empty buffer whose address may be anything) loads the buffer's own
+	// descriptor instead: aligned batches read no payload here (reading both
+	// blocks of every 4 KiB buffer cost C2 5 % per step).
+	const uint64_t safe = (uint64_t)(descs + min(b, n - 1u));
+	const uint64_t a0 = d.addr & ~(uint64_t)15;
+	const bool needA = d.len != 0 && (d.addr & 15u) != 0;          // head, or a tiny buffer's first block
+	const bool needT = d.len != 0 && ((d.addr + d.len) & 15u) != 0; // tail, or a tiny buffer's last block
+	const uint64_t aT0 = (d.addr + d.len - 1u) & ~(uint64_t)15;
+	const u32x4 vA = *(g_u32x4 *)(needA ? a0 : safe);
+	const u32x4 vT = *(g_u32x4 *)(needT ? aT0 : safe);
 	if (tid < 256)
 		t1[tid] = tv1;
 	if (tid < 384)
@@ -246,29 +272,46 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 			deltas[b] = dl;
 		}
 		if (rows == 0) {
-			// no full aligned piece: the whole buffer here (<= 30 bytes)
-			res = crc_bytes(t1, d.seed, d.addr, d.len);
-			if (COPY)
-				copy_bytes(d.addr, dl, d.len);
+			// no full aligned piece: the whole buffer here (<= 30 bytes, in
+			// block A and, if it crosses into the next block, block T)
+			// (two blocks only with an unaligned start and end: needA, needT)
+			res = d.seed;
+			if (d.len) {
+				const u32x4 v0 = needA ? vA : vT; // the block holding the first byte
+				const uint32_t o = (uint32_t)(d.addr - a0), e = (uint32_t)min((uint64_t)16u, o + (uint64_t)d.len);
+				res = crc_block(t1, res, v0, o, e);
+				if (aT0 != a0)
+					res = crc_block(t1, res, vT, 0, (uint32_t)(end - aT0));
+				if (COPY) {
+					copy_block(v0, o, e, a0 + dl);
+					if (aT0 != a0)
+						copy_block(vT, 0, (uint32_t)(end - aT0), aT0 + dl);
+				}
+			}
 		} else {
 			const uint64_t cs = (d.addr + 15) & ~(uint64_t)15;
 			const uint64_t ce = end & ~(uint64_t)15;
 			const uint32_t h = (uint32_t)(cs - d.addr), t = (uint32_t)(end - ce);
+			// head: the last h bytes of block A (= cs - 16); tail: the first t of block T (= ce)
 			if (COPY) {
-				copy_bytes(d.addr, dl, h);
-				copy_bytes(ce, dl, t);
+				copy_block(vA, 16u - h, 16u, a0 + dl);
+				copy_block(vT, 0u, t, aT0 + dl);
 			}
 			res = 0;
 			if (d.seed)
 				res ^= shift_bytes(powb, d.len, d.seed);
 			if (h)
-				res ^= shift_bytes(powb, (uint64_t)d.len - h, crc_bytes(t1, 0, d.addr, h));
+				res ^= shift_bytes(powb, (uint64_t)d.len - h, crc_block(t1, 0, vA, 16u - h, 16u));
 			if (t)
-				res ^= crc_bytes(t1, 0, ce, t);
-			const uint32_t vp = rows * 8u - (uint32_t)((ce - cs) >> 4);
-			core.vbase = ce - (uint64_t)PECH_ROW_BYTES * rows;
+				res ^= crc_block(t1, 0, vT, 0u, t);
+			// rows on the line grid (layout.h): vp leading virtual pieces in
+			// row 0, zt trailing ones in the last row
+			const uint64_t vb = cs & ~(uint64_t)(PECH_ROW_BYTES - 1u);
+			const uint32_t vp = (uint32_t)((cs - vb) >> 4);
+			const uint32_t zt = rows * 8u - (uint32_t)((ce - vb) >> 4);
+			core.vbase = vb;
 			core.rows = rows;
-			core.meta = PECH_META(b, vp, t);
+			core.meta = PECH_META(b, vp, t, zt);
 			cls = pech_size_class(rows);
 		}
 		out[b] = res;
@@ -430,14 +473,18 @@ extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
 // another group's rows and its state is ignored), `zoff` != 0 = the first
 // row's piece is a virtual zero (it may lie before the buffer, so row 0 is
 // loaded from ad + zoff -- the first real piece -- and zeroed), `m` = bytes
-// from the run's end to the buffer's end (final shift), `orig` = output slot.
+// from the run's end to the buffer's end (final shift; negative when the
+// run ends in the buffer's last row and its zt trailing virtual pieces
+// outnumber the tail bytes), `orig` = output slot, `zl` = the lane's piece
+// of the run's last row is a trailing virtual piece (read as zero, never
+// stored).
 // Uniform: T / nmin = max / min of nu over the active groups (T == 0: no
 // step), and the wave's cursor after the step.
 struct Step {
 	uint64_t ad;
-	uint32_t mp;  // rows after the run << 4 | tail bytes   (m = 128 rows + tail)
+	uint32_t mp;  // rows after the run << 4 | tail bytes   (m = 128 rows + tail - 16 zt)
 	uint32_t nl, nu;
-	uint32_t oz;  // orig | (zoff / 16) << 20               (zoff <= 112)
+	uint32_t oz;  // orig | (zoff / 16) << 20 | zl << 23 | zt << 24   (zoff <= 112, zt < 8)
 	uint32_t T, nmin;
 	uint32_t pos, lr, rem;
 	uint64_t dad; // fused copy: destination of this lane's piece in row 0 (ad + dst - src)
@@ -532,7 +579,10 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			S.ad = vb0 + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
 			S.nl = nn;
 			S.nu = nn;
-			S.oz = PECH_META_ORIG(meta0) | ((st == 0 && g8 < vp0) ? (vp0 - g8) << 20 : 0u);
+			const uint32_t zt0 = PECH_META_ZT(meta0);
+			const bool zl0 = st + nn == rows0 && g8 >= 8u - zt0; // this slice ends the buffer
+			S.oz = PECH_META_ORIG(meta0) | ((st == 0 && g8 < vp0) ? (vp0 - g8) << 20 : 0u) |
+			       (zl0 ? 1u << 23 : 0u) | (zt0 << 24);
 			S.mp = ((rows0 - st - nn) << 4) | PECH_META_TAIL(meta0);
 			S.T = q + (rm ? 1u : 0u);
 			S.nmin = q;
@@ -628,7 +678,9 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			}
 			S.nu = nu;
 			dl = mdl;
-			S.oz = PECH_META_ORIG(my.meta) | (zp << 20);
+			const uint32_t myzt = PECH_META_ZT(my.meta);
+			const bool zl = nu != 0 && mylr + nu == myrows && g8 >= 8u - myzt; // the run ends the buffer
+			S.oz = PECH_META_ORIG(my.meta) | (zp << 20) | (zl ? 1u << 23 : 0u) | (myzt << 24);
 			S.mp = ((myrows - mylr - nu) << 4) | PECH_META_TAIL(my.meta);
 #ifdef PECH_DEBUG_BOUNDS
 			const uint64_t bv = nu ? my.vbase : vb0;
@@ -652,7 +704,8 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 
 #define STEP_ZOFF(S) (((S).oz >> 16) & 0x70u) // (zoff/16) << 20 -> zoff
 #define STEP_ORIG(S) ((S).oz & 0xFFFFFu)
-#define STEP_M(S) ((uint64_t)((S).mp >> 4) * PECH_ROW_BYTES + ((S).mp & 15u))
+#define STEP_ZL(S) (((S).oz >> 23) & 1u)
+#define STEP_M(S) ((int64_t)((uint64_t)((S).mp >> 4) * PECH_ROW_BYTES + ((S).mp & 15u)) - 16 * (int64_t)((S).oz >> 24))
 
 // Ring discipline: row k of a step lives in ring slot k % PECH_U and the
 // lookahead is PECH_U-1 rows.  The iteration that consumes row k first issues
@@ -693,7 +746,7 @@ __device__ __forceinline__ void horner_row_pred(const uint32_t *lds, uint32_t lr
 // ending at the run's last row), shift it to the buffer's core end plus the
 // tail (m bytes), xor into out[orig].
 __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t s0, uint32_t s1, uint32_t s2,
-					   uint32_t s3, uint64_t m, bool active, uint32_t *out, uint32_t orig)
+					   uint32_t s3, int64_t m, bool active, uint32_t *out, uint32_t orig)
 {
 	uint32_t u = adv_tab(lds, L_TAB4, s0) ^ s1;
 	u = adv_tab(lds, L_TAB4, u) ^ s2;
@@ -707,8 +760,9 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 	u = adv_tab(lds, L_TAB32, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x102, 0xf, 0xf, true);
 	u = adv_tab(lds, L_TAB64, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x104, 0xf, 0xf, true);
 	uint32_t v = 0;
-	if (active && g8 == 0)
-		v = m ? shift_bytes(lds + L_POWB / 4u, m, u) : u;
+	if (active && g8 == 0) // m < 0: the run's trailing virtual zeros outweigh the tail
+		v = m > 0 ? shift_bytes(lds + L_POWB / 4u, (uint64_t)m, u)
+			  : (m < 0 ? gf2_mulmod(lds[L_XINV / 4u + (uint32_t)(-m)], u) : u);
 	// A split step (every active group on one buffer) folds its 8 group
 	// results in registers: one atomic per wave instead of 8 on one address.
 	const uint32_t o0 = uni(orig);
@@ -730,6 +784,18 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 	} else if (active && g8 == 0) {
 		atomicXor(out + orig, v);
 	}
+}
+
+// A trailing virtual piece (past the core's end, in the buffer's last row)
+// counts as zero; only the ragged and last blocks of a step can hold a run's
+// last row.
+__device__ __forceinline__ u32x4 zl_mask(const Step &S, uint32_t row, u32x4 v)
+{
+	return (STEP_ZL(S) && row == S.nu - 1u) ? (u32x4)(0u) : v;
+}
+__device__ __forceinline__ bool zl_keep(const Step &S, uint32_t row)
+{
+	return !(STEP_ZL(S) && row == S.nu - 1u);
 }
 
 // Fused copy: the consumed piece of row `row` of the lane's run goes to its
@@ -785,6 +851,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 	for (uint32_t k = 0; k < TPT; ++k)
 		tv[k] = c4[min(tid + k * PECH_MAIN_THREADS, NT4 - 1u)];
+	static_assert(PECH_MAIN_THREADS >= 128u, "inverse powers: one word per thread");
+	const uint32_t txi = consts[PECH_C_XINV + (tid & 127u)];
 	// (partials / nzs hold PECH_MAX_CHUNKS entries, lrs whole chunks)
 	u32x4 pv4[4], nv4[4], lr4[4];
 #pragma unroll
@@ -947,6 +1015,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	for (uint32_t k = 0; k < TPT; ++k)
 		if (tid + k * PECH_MAIN_THREADS < NT4)
 			*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
+	if (tid < 128u)
+		lds[L_XINV / 4u + tid] = txi;
 	if (tid < PECH_DEFER_SLOTS) {
 		lds[L_DEFER / 4u + tid] = PECH_DEFER_EMPTY;
 		lds[L_DEFER / 4u + PECH_DEFER_SLOTS + tid] = 0u;
@@ -988,8 +1058,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] =
 					LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
-				horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
-				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)));
+				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+				st_piece<COPY>(S, r + i, ring[i],
+					       r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)) && zl_keep(S, r + i));
 			}
 		}
 		// last block: its first load is this step's last row, the rest
@@ -997,8 +1068,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
 		const Step N = plan_step<COPY>(cores, deltas, lds, S.pos, S.lr, S.rem, lane, g8, grp);
-		horner_row_pred(lds, lreg, ring[0], r < S.nu, s0, s1, s2, s3);
-		st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_ZOFF(S)));
+		horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
+		st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_ZOFF(S)) && zl_keep(S, r));
 		// Branch-free on purpose: with no next step the prefetch re-reads
 		// this step's last row (valid memory, never used).  An if/else here
 		// let LLVM sink the shared Horner code into a join block, which
@@ -1009,8 +1080,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 		for (uint32_t i = 1; i < U; ++i) {
 			ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
-			horner_row_pred(lds, lreg, ring[i], r + i < S.nu, s0, s1, s2, s3);
-			st_piece<COPY>(S, r + i, ring[i], r + i < S.nu);
+			horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+			st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && zl_keep(S, r + i));
 		}
 #ifdef PECH_DEBUG_BOUNDS
 		{ // debug build: an active group's output slot must lie in this launch's slots
@@ -1142,6 +1213,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.12 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.13 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
 }

@@ -38,11 +38,12 @@ WAVES_PER_WG = C["PECH_MAIN_WAVES"]
 
 
 def core_rows(addr, ln):
+    """rows (128-byte lines) holding the core (layout.h pech_core_rows)"""
     cs = (addr + 15) & ~15
     ce = (addr + ln) & ~15
     if ce <= cs:
         return 0
-    return (((ce - cs) >> 4) + 7) >> 3
+    return (ce - (cs & ~127) + 127) >> 7
 
 
 def size_class(rows):
@@ -73,9 +74,11 @@ def plan(descs, rng=None):
                 continue
             cs = (addr + 15) & ~15
             ce = (addr + ln) & ~15
-            vp = rows * 8 - ((ce - cs) >> 4)
+            vbase = cs & ~127  # rows on the line grid
+            vp = (cs - vbase) >> 4
+            zt = rows * 8 - ((ce - vbase) >> 4)
             t = addr + ln - ce
-            items.append(dict(vbase=ce - ROW * rows, rows=rows, orig=b, vp=vp, tail=t, cs=cs, ce=ce,
+            items.append(dict(vbase=vbase, rows=rows, orig=b, vp=vp, zt=zt, tail=t, cs=cs, ce=ce,
                               cls=size_class(rows)))
         order = []
         for cls in range(13):
@@ -240,9 +243,12 @@ def walk(cores, nzs, pos, lr, rem, U, events):
                         loads, used = run_rows_loads(U, nn, nn, zoff, T, q)
                         for row, z in loads:
                             events.append(("load", cd, cd["vbase"] + (st + row) * ROW + 16 * g8 + (zoff if z else 0)))
+                        zl = st + nn == rows0 and g8 >= 8 - cd["zt"]
                         for row in used:
-                            events.append(("use", cd["orig"], st + row, g8, zoff != 0 and row == 0))
-                    events.append(("finish", cd["orig"], st + nn, (rows0 - st - nn) * ROW + cd["tail"]))
+                            events.append(("use", cd["orig"], st + row, g8,
+                                           (zoff != 0 and row == 0) or (zl and row == nn - 1)))
+                    events.append(("finish", cd["orig"], st + nn,
+                                   (rows0 - st - nn) * ROW + cd["tail"] - 16 * cd["zt"]))
                 rem -= P
                 if P == avail0:
                     pos += 1
@@ -282,10 +288,13 @@ def walk(cores, nzs, pos, lr, rem, U, events):
                         loads, used = run_rows_loads(U, nl, nu, zoff, T, nmin)
                         for row, z in loads:
                             events.append(("load", buf, base + row * ROW + (zoff if z else 0)))
+                        zl = nu != 0 and mylr + nu == myrows and g8 >= 8 - my["zt"]
                         for row in used:
-                            events.append(("use", my["orig"], mylr + row, g8, zoff != 0 and row == 0))
+                            events.append(("use", my["orig"], mylr + row, g8,
+                                           (zoff != 0 and row == 0) or (zl and row == nu - 1)))
                     if nu:
-                        events.append(("finish", my["orig"], mylr + nu, (myrows - mylr - nu) * ROW + my["tail"]))
+                        events.append(("finish", my["orig"], mylr + nu,
+                                       (myrows - mylr - nu) * ROW + my["tail"] - 16 * my["zt"]))
                 rem -= used_rows
                 if rem:
                     pos += kcut

@@ -1,6 +1,8 @@
 """CPU checks of the main kernel's work decomposition through the shadow
-model (tests/kernel_model.py): loads stay inside real buffer cores, every
-core row is consumed exactly once, shifts target the buffer end."""
+model (tests/kernel_model.py): loads stay inside the lines holding each
+buffer's core (never before its first real piece), every row piece is
+consumed exactly once, the pieces outside the core count as zeros, and
+shifts target the buffer end."""
 import collections
 import random
 
@@ -21,17 +23,19 @@ def check(descs, ncu=4, seed=0, weights=None, U=None):
     for e in ev:
         if e[0] == "load":
             _, buf, a = e
-            assert buf["cs"] <= a and a + 16 <= buf["ce"], (buf, a)
+            # past ce only inside the core's last line (trailing virtual pieces)
+            assert buf["cs"] <= a and a + 16 <= buf["vbase"] + buf["rows"] * KM.ROW, (buf, a)
+            assert a % KM.ROW // 16 == (a - buf["vbase"]) % KM.ROW // 16  # rows on the line grid
         elif e[0] == "use":
             _, orig, row, g8, virt = e
             c = byorig[orig]
             used[(orig, row, g8)] += 1
             piece = row * 8 + g8
-            assert virt == (piece < c["vp"]), (orig, row, g8)
+            assert virt == (piece < c["vp"] or piece >= c["rows"] * 8 - c["zt"]), (orig, row, g8)
         elif e[0] == "finish":
             _, orig, endrow, m = e
             c = byorig[orig]
-            assert m == (c["rows"] - endrow) * KM.ROW + c["tail"]
+            assert m == (c["rows"] - endrow) * KM.ROW + c["tail"] - 16 * c["zt"]
     for orig, c in byorig.items():
         for row in range(c["rows"]):
             for g8 in range(8):
