@@ -159,6 +159,34 @@ def test_c3_shape_parity(torch_dev, P):
     assert np.array_equal(got, O.crcs(host, offs, [L] * n))
 
 
+@pytest.mark.parametrize("config", ["c3", "c4", "c2-odd"])
+def test_full_size_batch_parity(torch_dev, P, config):
+    """BASELINE configs at their full per-GPU size, every output checked
+    against the oracle: C3 = 256 x 4 MiB (1 GiB, the bench's batch), C4 =
+    65,536 x 4 KiB + 4,096 x 64 KiB + 256 x 1 MiB + 64 x 4 MiB shuffled with
+    seed 42 (1 GiB, bench.py's c4_sizes), and bench.py's unaligned c2-odd
+    (65,536 x 4,100 B back to back), random seeds."""
+    torch, dev = torch_dev
+    if config == "c3":
+        sizes = [4 << 20] * 256
+    elif config == "c2-odd":
+        sizes = [4100] * 65536
+    else:
+        sizes = [4096] * 65536 + [65536] * 4096 + [1 << 20] * 256 + [4 << 20] * 64
+        np.random.default_rng(42).shuffle(sizes)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    total = int(np.sum(sizes))
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    buf = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    seeds = [int(x) for x in np.random.default_rng(8).integers(0, 1 << 32, len(sizes))]
+    got = dev_crcs(torch, P, buf, offs, sizes, seeds)
+    host = buf.cpu().numpy()
+    del buf
+    want = O.crcs(host, offs, sizes, seeds)
+    assert np.array_equal(got, want), int(np.sum(got != want))
+
+
 def test_c4_mixed_sizes_parity(torch_dev, P):
     # config 4 mix (4 KiB / 64 KiB / 1 MiB / 4 MiB), shuffled, scaled to 128 MiB
     torch, dev = torch_dev
