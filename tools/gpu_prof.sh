@@ -26,5 +26,6 @@ for C in ${CFGS:-c3}; do
   fi
   python3 tools/pmc_traffic.py $(find gpurun_out/prof_${C}_fetch -name "*counter_collection.csv" | head -1) \
     $C "$TAG" gpurun_out/${C}_traffic.json $W || echo "traffic json failed"
+  python3 tools/trim_prof.py gpurun_out/prof_${C}_trace gpurun_out/prof_${C}_fetch gpurun_out/prof_${C}_write
 done
 exit 0
