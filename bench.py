@@ -405,6 +405,17 @@ def dropin_latency(P):
     res = json.loads(r.stdout.decode().strip().splitlines()[-1])
     res["path"] = ("crc32c(0, buf, n) from pageable memory, synchronous, called from C; host = default "
                    "routing (<= 4 MiB on the host routine), gpu = crc32c_set_cpu_max(0), ref = reference loop")
+    # BASELINE config 1 (fio 4 KiB OP_WRITE against a pech-osd) needs fio and a
+    # Ceph monitor, absent here.  Its checksum work per operation, from the
+    # per-call latencies above: the request's header (49 B, messenger.c:2714),
+    # front (~200 B, :2641) and 4 KiB data (:2677 via :1729), and the reply's
+    # header (:1403) and front (:1412); a write reply carries no data.
+    sz = res.get("sizes", {})
+    if all(k in sz for k in ("49", "200", "4096")):
+        per_op = {k: round(2 * sz["49"][k] + 2 * sz["200"][k] + sz["4096"][k], 4) for k in ("host", "ref")}
+        res["c1_per_op"] = {"calls": "2 x header 49 B + 2 x front 200 B + data 4096 B", "unit": "us",
+                            "drop_in": per_op["host"], "reference": per_op["ref"],
+                            "note": "derived from the per-call latencies; the fio plumbing itself is not run"}
     return res
 
 
