@@ -71,7 +71,9 @@ struct crc32c_desc {
  * CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES: the batch is split into contiguous,
  * byte-balanced shards, one per visible GPU, each read in place over its own
  * host link; all shards are issued from the calling thread before any is
- * waited for (pech's one thread drives a whole node).  Every
+ * waited for (pech's one thread drives a whole node).  A
+ * buffer of at least 16 MiB that exceeds one GPU's share of the batch is cut
+ * into per-GPU segments whose CRCs are combined on the host.  Every
  * buffer must be mapped on every GPU (hipHostMalloc / crc32c_pages memory);
  * otherwise -EINVAL and nothing is launched.  Other flag combinations with
  * CRC32C_F_ALL_DEVICES are -EINVAL.

@@ -474,6 +474,15 @@ static unsigned int launch_take(const unsigned int *lens, unsigned int i0, unsig
 // shards per device, on its two slots -- how the 1-GPU tests split a batch).
 // Every shard's sub-batch is enqueued before any is waited for, so the GPUs
 // read their host links concurrently from this one thread.
+static int shard_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds, uint32_t *out,
+			unsigned int n, const int *devs, int nd);
+
+// SURVEY 8(e), the optional split: a buffer larger than one device's fair
+// share of the batch (and at least PECH_SPLIT_MIN_BYTES) is cut into
+// per-device segments of whole 4 KiB pages, the first carrying the seed; the
+// segment CRCs are combined on the host, R(s, A || B) = A_|B|(R(s, A)) ^
+// R(0, B), so one huge buffer still keeps every GPU's host link busy.
+#define PECH_SPLIT_MIN_BYTES (16u << 20)
 static int multi_device_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
 			       uint32_t *out, unsigned int n)
 {
@@ -495,18 +504,69 @@ static int multi_device_pinned(const void *const *bufs, const unsigned int *lens
 	}
 	int ndev_all = 0;
 	HIP_TRY(hipGetDeviceCount(&ndev_all));
-	int slot[64], used[64] = {0};
+	int used[64] = {0};
 	for (int k = 0; k < nd; ++k) {
 		if (devs[k] < 0 || devs[k] >= ndev_all || devs[k] >= 64 || used[devs[k]] >= 2) {
 			set_err("crc32c_batch: bad device list (PECH_DEVICES)");
 			return -EINVAL;
 		}
-		slot[k] = used[devs[k]]++;
+		used[devs[k]]++;
 	}
 	if (nd == 0) {
 		set_err("no usable GPU");
 		return -ENODEV;
 	}
+	uint64_t total = 0;
+	for (unsigned int i = 0; i < n; ++i)
+		total += lens[i];
+	const uint64_t fair = total / (uint64_t)nd;
+	bool split = false;
+	for (unsigned int i = 0; i < n && nd > 1 && !split; ++i)
+		split = lens[i] >= PECH_SPLIT_MIN_BYTES && lens[i] > fair;
+	if (!split)
+		return shard_pinned(bufs, lens, seeds, out, n, devs, nd);
+	struct Seg {
+		unsigned int orig;
+		uint64_t after; // bytes of the buffer after this segment
+	};
+	std::vector<const void *> sb;
+	std::vector<unsigned int> sl;
+	std::vector<uint32_t> ss;
+	std::vector<Seg> sg;
+	for (unsigned int i = 0; i < n; ++i) {
+		const uint32_t seed = seeds ? seeds[i] : 0u;
+		unsigned int k = 1;
+		if (lens[i] >= PECH_SPLIT_MIN_BYTES && lens[i] > fair)
+			k = (unsigned int)std::min<uint64_t>((uint64_t)nd, (lens[i] + fair - 1) / std::max<uint64_t>(fair, 1));
+		const uint64_t piece = ((uint64_t)lens[i] / k) & ~(uint64_t)4095;
+		uint64_t off = 0;
+		for (unsigned int j = 0; j < k; ++j) {
+			const uint64_t len = j + 1 == k ? lens[i] - off : piece;
+			sb.push_back((const char *)bufs[i] + off);
+			sl.push_back((unsigned int)len);
+			ss.push_back(j == 0 ? seed : 0u);
+			sg.push_back(Seg{i, lens[i] - off - len});
+			off += len;
+		}
+	}
+	std::vector<uint32_t> so(sb.size());
+	const int rc = shard_pinned(sb.data(), sl.data(), ss.data(), so.data(), (unsigned int)sb.size(), devs, nd);
+	if (rc)
+		return rc;
+	for (unsigned int i = 0; i < n; ++i)
+		out[i] = 0;
+	for (size_t j = 0; j < sg.size(); ++j)
+		out[sg[j].orig] ^= sg[j].after ? gf2_shift(so[j], sg[j].after) : so[j];
+	return 0;
+}
+
+// Contiguous byte-balanced shards of the batch, one per listed device.
+static int shard_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds, uint32_t *out,
+			unsigned int n, const int *devs, int nd)
+{
+	int slot[64], used[64] = {0};
+	for (int k = 0; k < nd; ++k)
+		slot[k] = used[devs[k]]++;
 	// shard k = buffers [cut[k], cut[k+1]): the first buffer whose byte prefix reaches k/nd of the total
 	std::vector<uint64_t> pre(n + 1, 0);
 	for (unsigned int i = 0; i < n; ++i)

@@ -399,6 +399,37 @@ def test_batch_pinned_all_devices(torch_dev, P, monkeypatch, devices):
     assert L.crc32c_batch(p1, l1, None, out, 1, P.F_PINNED | P.F_ALL_DEVICES) == -22
 
 
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+def test_batch_pinned_all_devices_splits_huge_buffer(torch_dev, P, monkeypatch, devices):
+    """A buffer larger than one device's share (>= 16 MiB) is cut into
+    per-device segments whose CRCs combine on the host (SURVEY 8e's optional
+    split).  Three "devices" on one GPU: two slots per device at most, so
+    "0,0,0" must be refused; "0,0" splits."""
+    torch, dev = torch_dev
+    from pech_amd import _lib
+
+    monkeypatch.setenv("PECH_DEVICES", devices)
+    rng = np.random.default_rng(31)
+    lens = np.array([(100 << 20) + 12345, 5000, 0, 17, (20 << 20) + 3, 4096], dtype=np.int64)
+    host = torch.empty(int(lens.sum()) + 64, dtype=torch.uint8).pin_memory()
+    data = rng.integers(0, 256, host.numel(), dtype=np.uint8)
+    host.copy_(torch.from_numpy(data))
+    offs = np.concatenate([[5], 5 + np.cumsum(lens)[:-1]])
+    seeds = rng.integers(0, 1 << 32, len(lens), dtype=np.uint64)
+    n = len(lens)
+    ptrs = (ctypes.c_void_p * n)(*[host.data_ptr() + int(o) for o in offs])
+    cl = (ctypes.c_uint * n)(*[int(x) for x in lens])
+    cs = (ctypes.c_uint32 * n)(*[int(x) for x in seeds])
+    out = (ctypes.c_uint32 * n)()
+    L = _lib.lib()
+    rc = L.crc32c_batch(ptrs, cl, cs, out, n, P.F_PINNED | P.F_ALL_DEVICES)
+    if devices == "0,0,0":
+        assert rc == -22
+        return
+    assert rc == 0, L.crc32c_last_error()
+    assert np.array_equal(np.frombuffer(out, dtype=np.uint32), O.crcs(data, offs, lens, seeds))
+
+
 def test_batch_device_aliasing_beyond_launch_limit(torch_dev, P):
     # 60,000 descriptors over ONE 5 MiB device buffer: 293 GiB of payload,
     # past the 256 GiB per-launch cap (rows are counted in 32 bits), so
