@@ -11,6 +11,12 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 dev = torch.device("cuda:0")
 if cfg == "c3":
     sizes = np.full(256, 4 << 20, dtype=np.int64)
+elif cfg == "c4":  # bench.py's c4_sizes: equal bytes per class, shuffled with seed 42
+    sizes = [4096] * 65536 + [65536] * 4096 + [1 << 20] * 256 + [4 << 20] * 64
+    np.random.default_rng(42).shuffle(sizes)
+    sizes = np.asarray(sizes, dtype=np.int64)
+elif cfg == "c2-1g":
+    sizes = np.full(262144, 4096, dtype=np.int64)
 else:
     sizes = np.full(65536, 4096, dtype=np.int64)
 offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
@@ -49,6 +55,9 @@ for nm, a, b in (("entry->scan", ent, tscan), ("scan->find", tscan, tfind), ("fi
 print("start us p50/p99/max: %.1f %.1f %.1f" % (pct(s,50)/100, pct(s,99)/100, s.max()/100))
 print("end   us p1/p10/p50/p90/max: %.1f %.1f %.1f %.1f %.1f" % (pct(e,1)/100, pct(e,10)/100, pct(e,50)/100, pct(e,90)/100, e.max()/100))
 print("mean wave busy / span: %.3f" % float(((e - s) / span).mean()))
+busy = (e - s) / 100
+print("busy us p1/p10/p50/p90/p99/max: %.1f %.1f %.1f %.1f %.1f %.1f" % (pct(busy, 1), pct(busy, 10), pct(busy, 50),
+                                                                        pct(busy, 90), pct(busy, 99), busy.max()))
 hist, edges = np.histogram(e / 100, bins=12)
 print("end-time histogram (us):", [(round(float(edges[i]),1), int(hist[i])) for i in range(len(hist))])
 
