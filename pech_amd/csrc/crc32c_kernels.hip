@@ -527,12 +527,12 @@ static_assert(PECH_MAIN_WAVES % 4 == 0 && PECH_MAIN_WAVES <= 16, "waves per work
 
 // Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
 // the destination offset of each group's buffer (deltas[orig], scalar loads).
-// PRE: `pre` holds cores[ppos + grp] (loaded at kernel entry); a step that
+// PRE: `spec` holds cores[ppos + grp] (loaded at kernel entry); a step that
 // starts at ppos takes its descriptors from it instead of loading them.
 template <bool COPY, bool PRE = false>
 __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
 					  const uint32_t *lds, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
-					  uint32_t g8, uint32_t grp, const pech_core &pre = pech_core{}, uint32_t ppos = 0)
+					  uint32_t g8, uint32_t grp, const pech_core &spec = pech_core{}, uint32_t ppos = 0)
 {
 	Step S;
 	int64_t dl = 0;
@@ -558,7 +558,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 		const bool hit = PRE && pos == ppos; // wave-uniform
 		pech_core cd;
 		if (hit)
-			cd = pre; // lanes 0-7 (group 0) hold cores[pos]; uni() reads lane 0
+			cd = spec; // lanes 0-7 (group 0) hold cores[pos]; uni() reads lane 0
 		else
 			cd = cores[pos];
 #ifdef PECH_DEBUG_BOUNDS
@@ -608,32 +608,32 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
 			int64_t mdl = 0;
 			if (hit) {
-				vlo = (uint32_t)pre.vbase;
-				vhi = (uint32_t)(pre.vbase >> 32);
-				mrows = pre.rows;
-				mmeta = pre.meta;
+				vlo = (uint32_t)spec.vbase;
+				vhi = (uint32_t)(spec.vbase >> 32);
+				mrows = spec.rows;
+				mmeta = spec.meta;
 				if (COPY) {
 					const uint32_t pj = pos + grp;
 					const bool okj = (pj & 1023u) < nzc && (pj >> 10) == c;
-					mdl = deltas[okj ? PECH_META_ORIG(pre.meta) : 0u];
+					mdl = deltas[okj ? PECH_META_ORIG(spec.meta) : 0u];
 				}
 			} else {
 #pragma unroll
-			for (uint32_t j = 0; j < 8; ++j) {
-				const pech_core dj = cores[pos + j];
-				const bool mine = grp == j;
-				vlo = mine ? uni((uint32_t)dj.vbase) : vlo;
-				vhi = mine ? uni((uint32_t)(dj.vbase >> 32)) : vhi;
-				mrows = mine ? uni(dj.rows) : mrows;
-				mmeta = mine ? uni(dj.meta) : mmeta;
-				if (COPY) {
-					// entries past the chunk are garbage: never index with them
-					const uint32_t pj = pos + j;
-					const bool okj = (pj & 1023u) < nzc && (pj >> 10) == c;
-					const int64_t dj_dl = deltas[okj ? PECH_META_ORIG(uni(dj.meta)) : 0u];
-					mdl = mine ? dj_dl : mdl;
+				for (uint32_t j = 0; j < 8; ++j) {
+					const pech_core dj = cores[pos + j];
+					const bool mine = grp == j;
+					vlo = mine ? uni((uint32_t)dj.vbase) : vlo;
+					vhi = mine ? uni((uint32_t)(dj.vbase >> 32)) : vhi;
+					mrows = mine ? uni(dj.rows) : mrows;
+					mmeta = mine ? uni(dj.meta) : mmeta;
+					if (COPY) {
+						// entries past the chunk are garbage: never index with them
+						const uint32_t pj = pos + j;
+						const bool okj = (pj & 1023u) < nzc && (pj >> 10) == c;
+						const int64_t dj_dl = deltas[okj ? PECH_META_ORIG(uni(dj.meta)) : 0u];
+						mdl = mine ? dj_dl : mdl;
+					}
 				}
-			}
 			}
 			pech_core my;
 			my.vbase = ((uint64_t)vhi << 32) | vlo;
