@@ -33,3 +33,21 @@ def test_single_thread_matches_process_per_gpu_schema():
     assert abs(a["value"] - b["value"]) / a["value"] < 0.10, (a["value"], b["value"])
     # two shards on one GPU share its HBM: about one GPU's rate in aggregate
     assert 0.7 < c["value"] / a["value"] < 1.3, (a["value"], c["value"])
+
+
+def test_torchrun_two_ranks_real_kernels():
+    """bench.py's N>1 driver under torchrun with the real kernels: two ranks
+    share GPU 0 over gloo (PECH_BENCH_BACKEND=gloo; the driver's N>1 runs use
+    RCCL with one GPU per rank).  Rendezvous, barriers, MAX-over-ranks timing
+    and rank 0's single JSON line; each rank checksums its own shard."""
+    env = dict(os.environ, PECH_BENCH_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2", *COMMON],
+                       cwd=REPO, capture_output=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, lines  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    assert d["config"]["parallelism"].startswith("shard2")
+    assert "cpu_baseline" not in d  # rank 0 at N=1 only
