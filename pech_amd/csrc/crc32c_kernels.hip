@@ -37,7 +37,7 @@
 #define PECH_U 8 // rows in flight per lane
 #endif
 #ifndef PECH_U_COPY
-#define PECH_U_COPY 8 // rows in flight per lane, fused-copy variant
+#define PECH_U_COPY 12 // rows per block, fused-copy variant (block discipline, 128 VGPRs)
 #endif
 #ifndef PECH_MAIN_WAVES
 #define PECH_MAIN_WAVES 16 // waves per main-kernel workgroup (one workgroup per CU)
@@ -1044,6 +1044,26 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			if (nstep == 0 && (blk == nblk / 4u || blk == nblk / 2u || blk == 3u * nblk / 4u))
 				tq[blk == nblk / 4u ? 0 : (blk == nblk / 2u ? 1 : 2)] = __builtin_amdgcn_s_memrealtime();
 #endif
+			if constexpr (COPY) {
+				// Block discipline for the fused copy: the block's last row, its U
+				// Horner rows, its U stores together, then the next block's first
+				// U-1 rows.  vmcnt counts stores too and retires in issue order, so
+				// in the rotating ring every load waited behind the stores issued
+				// after it (half the lookahead); here a load waits only behind
+				// stores issued before it.  Measured: C3 copy 449-465 -> 389-397 us
+				// per launch (profiles/r02/ab_copy_block.txt).
+				ring[U - 1] = LD_PIECE(S, base + (U - 1) * PECH_ROW_BYTES, 2);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_ZOFF(S)));
+#pragma unroll
+				for (uint32_t i = 0; i + 1 < U; ++i)
+					ring[i] = LD_PIECE(S, base + (U + i) * PECH_ROW_BYTES, 2);
+				continue;
+			}
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
@@ -1054,6 +1074,20 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// ragged blocks: clamped prefetch, predicated update
 		for (; blk + 1 < nblk; ++blk) {
 			const uint32_t r = blk * U;
+			if constexpr (COPY) { // block discipline (see the full blocks), clamped and predicated
+				ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 3);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					st_piece<COPY>(S, r + i, ring[i],
+						       r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)) && zl_keep(S, r + i));
+#pragma unroll
+				for (uint32_t i = 0; i + 1 < U; ++i)
+					ring[i] = LD_PIECE(S, row_addr(S.ad, min(r + U + i, last), STEP_ZOFF(S)), 3);
+				continue;
+			}
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] =
@@ -1068,20 +1102,35 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
 		const Step N = plan_step<COPY>(cores, deltas, lds, S.pos, S.lr, S.rem, lane, g8, grp);
-		horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
-		st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_ZOFF(S)) && zl_keep(S, r));
-		// Branch-free on purpose: with no next step the prefetch re-reads
-		// this step's last row (valid memory, never used).  An if/else here
-		// let LLVM sink the shared Horner code into a join block, which
-		// cost ring-register copies behind a vmcnt(0) at every step end.
-		const bool more = N.T != 0;
-		const Step &L = more ? N : S;
-		const uint32_t lrow0 = more ? 0u : last, lmax = more ? N.nl - 1u : last;
+		if constexpr (COPY) { // block discipline: this block's rows and stores, then the next step's loads
+			const bool more = N.T != 0;
+			const Step &L = more ? N : S;
+			const uint32_t lrow0 = more ? 0u : last, lmax = more ? N.nl - 1u : last;
 #pragma unroll
-		for (uint32_t i = 1; i < U; ++i) {
-			ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
-			horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
-			st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && zl_keep(S, r + i));
+			for (uint32_t i = 0; i < U; ++i)
+				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i)
+				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)) && zl_keep(S, r + i));
+#pragma unroll
+			for (uint32_t i = 1; i < U; ++i)
+				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
+		} else {
+			horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
+			st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_ZOFF(S)) && zl_keep(S, r));
+			// Branch-free on purpose: with no next step the prefetch re-reads
+			// this step's last row (valid memory, never used).  An if/else here
+			// let LLVM sink the shared Horner code into a join block, which
+			// cost ring-register copies behind a vmcnt(0) at every step end.
+			const bool more = N.T != 0;
+			const Step &L = more ? N : S;
+			const uint32_t lrow0 = more ? 0u : last, lmax = more ? N.nl - 1u : last;
+#pragma unroll
+			for (uint32_t i = 1; i < U; ++i) {
+				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
+				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && zl_keep(S, r + i));
+			}
 		}
 #ifdef PECH_DEBUG_BOUNDS
 		{ // debug build: an active group's output slot must lie in this launch's slots
@@ -1213,6 +1262,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.13 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
-		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES);
+	return "pech_crc32c 0.14 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY);
 }

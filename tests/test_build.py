@@ -103,32 +103,58 @@ def test_row_loops_never_drain_the_ring(device_asm, kernel="pech_crc32c_main"):
         assert len(movs) <= 8, (name, len(movs))
 
 
-@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy"])
-def test_loops_with_ring_loads_never_wait_for_zero(device_asm, kernel):
-    """Loop-level form of the check (the fused-copy kernel's loops span
-    several basic blocks): every loop -- from a "Loop Header" label to the
-    last branch back to it -- that issues ring loads has only counted
-    vmcnt waits."""
-    asm, _ = device_asm
-    lines = kernel_body(asm, kernel).split("\n")
+def _loop_regions(body):
+    """Every loop of a kernel body, from its "Loop Header" label to the last
+    branch back to it (the fused-copy kernel's loops span several basic
+    blocks): [(label, lines)]."""
+    lines = body.split("\n")
     heads = []  # (line, label): the header comment sits on the label's line or the next one
     for i, l in enumerate(lines):
         m = re.match(r"^(\.LBB\w+):", l)
         if m and ("Loop Header" in l or (i + 1 < len(lines) and "Loop Header" in lines[i + 1]
                                          and not lines[i + 1].lstrip().startswith("."))):
             heads.append((i, m.group(1)))
-    checked = 0
+    out = []
     for i0, label in heads:
         pat = re.compile(r"^\s*s_(?:cbranch_\w+|branch)\s+%s\b" % re.escape(label))
         back = [i for i, l in enumerate(lines) if i > i0 and pat.search(l)]
-        if not back:
-            continue
-        region = lines[i0:back[-1] + 1]
+        if back:
+            out.append((label, lines[i0:back[-1] + 1]))
+    return out
+
+
+def test_loops_with_ring_loads_never_wait_for_zero(device_asm):
+    """Loop-level form of the check: every loop of the CRC kernel that issues
+    ring loads has only counted vmcnt waits."""
+    asm, _ = device_asm
+    checked = 0
+    for label, region in _loop_regions(kernel_body(asm, "pech_crc32c_main")):
         if sum("global_load_dwordx4" in l for l in region) < 4:
             continue
         checked += 1
-        assert not [l for l in region if "vmcnt(0)" in l], (kernel, label)
-    assert checked >= 1, (kernel, checked)  # the step loop, which holds every row loop
+        assert not [l for l in region if "vmcnt(0)" in l], label
+    assert checked >= 1, checked  # the step loop, which holds every row loop
+
+
+def test_copy_row_loops_group_their_stores(device_asm):
+    """The fused-copy kernel's block discipline (vmcnt counts stores and
+    retires in issue order, so a store issued between two ring loads makes
+    the later load's wait cover it): in each innermost row loop the stores
+    come as one run, between the block's Horner rows and the next block's
+    loads -- at most one load->store and one store->load switch per
+    iteration, where the rotating ring had one per row."""
+    asm, _ = device_asm
+    U = int(re.search(r"#define PECH_U_COPY (\d+)", open(SRC).read()).group(1))
+    rowloops = []
+    for label, region in _loop_regions(kernel_body(asm, "pech_crc32c_main_copy")):
+        ops = [("L" if "global_load_dwordx4" in l else "S") for l in region
+               if "global_load_dwordx4" in l or "global_store_dwordx4" in l]
+        if ops.count("L") >= U - 1 and ops.count("S") >= U and ops.count("L") <= 2 * U:
+            rowloops.append((label, ops))
+    assert len(rowloops) >= 2, [(lb, "".join(o)) for lb, o in rowloops]  # the full and the ragged block loops
+    for label, ops in rowloops:
+        switches = sum(a != b for a, b in zip(ops, ops[1:]))
+        assert switches <= 2, (label, "".join(ops))
 
 
 def _hipcc():

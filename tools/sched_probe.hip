@@ -508,6 +508,39 @@ __global__ __launch_bounds__(1024, 1) void k_copy_wide(const uint8_t *p, uint8_t
 	}
 }
 
+// static shares read with the rows interleaved over the groups: group g walks
+// rows g, g+8, g+16, ... of the wave's share, so each wave-instruction reads
+// 8 consecutive rows (1 KiB contiguous, the grid's per-instruction footprint)
+// inside the persistent shape; DD rows in flight per lane
+template <int DD>
+__global__ __launch_bounds__(1024, 1) void k_wide(const uint8_t *p, uint32_t R, uint32_t *out)
+{
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const uint32_t n = r1 - r0, T = (n + 7u) / 8u;
+	const uint32_t ng = n > grp ? (n - grp + 7u) / 8u : 0u;
+	if (T == 0)
+		return;
+	const uint32_t last = ng ? ng - 1u : 0u, base = ng ? r0 + grp : r0;
+	u32x4 acc = (u32x4)(0u), ring[DD];
+#pragma unroll
+	for (int i = 0; i + 1 < DD; ++i)
+		ring[i] = ld(p, base + 8u * min((uint32_t)i, last), g8);
+	for (uint32_t j = 0; j < T; j += DD) {
+#pragma unroll
+		for (int i = 0; i < DD; ++i) {
+			ring[(i + DD - 1) % DD] = ld(p, base + 8u * min(j + i + DD - 1, last), g8);
+			if (j + i < ng)
+				acc ^= ring[i];
+		}
+	}
+	const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+	if (x == 0x12345678u)
+		out[w] = x;
+}
+
 // plain one-element-per-thread float4 copy over a large grid (not persistent)
 template <bool NT>
 __global__ __launch_bounds__(256) void k_copy_grid(const uint8_t *p, uint8_t *q, uint64_t n16)
@@ -981,6 +1014,35 @@ int main(int argc, char **argv)
 			printf("%s  {\"probe\": \"static + %u extra WGs over the last %.1f%% (idle %u us)\", \"us\": %.2f, \"GBps\": %.1f}",
 			       sep(), ex[v].X, ex[v].permille / 10.0, ex[v].idle, tot / reps * 1e3, bytes / (tot / reps * 1e-3) / 1e9);
 		}
+	}
+	if (!strcmp(which, "wide")) { // group-sliced static vs row-interleaved static vs the grid, two passes
+		const char *names[] = {"read static (group slices)", "read static wide D8 (rows interleaved over groups)",
+				       "read static wide D12", "read grid float4 nt"};
+		for (int pass = 0; pass < 2; ++pass)
+			for (int v = 0; v < 4; ++v) {
+				float tot = 0;
+				for (int r = -2; r < reps; ++r) {
+					CHECK(hipEventRecord(e0, 0));
+					const uint8_t *src = buf[(r + 4) % 2];
+					if (v == 0)
+						hipLaunchKernelGGL(k_sched<0>, dim3(ncu), dim3(1024), 0, 0, src, R, ctl, 0u, out, nsteal);
+					else if (v == 1)
+						hipLaunchKernelGGL(k_wide<8>, dim3(ncu), dim3(1024), 0, 0, src, R, out);
+					else if (v == 2)
+						hipLaunchKernelGGL(k_wide<12>, dim3(ncu), dim3(1024), 0, 0, src, R, out);
+					else
+						hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(bytes / 16 / 256)), dim3(256), 0, 0,
+								   src, (uint64_t)(bytes / 16), out);
+					CHECK(hipEventRecord(e1, 0));
+					CHECK(hipEventSynchronize(e1));
+					float ms;
+					CHECK(hipEventElapsedTime(&ms, e0, e1));
+					if (r >= 0)
+						tot += ms;
+				}
+				printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}", sep(), names[v], tot / reps * 1e3,
+				       bytes / (tot / reps * 1e-3) / 1e9);
+			}
 	}
 	if (!strcmp(which, "grid")) { // the best shapes measured: one float4 per thread, non-persistent grid, nt
 		for (int v = 0; v < 2; ++v) {
