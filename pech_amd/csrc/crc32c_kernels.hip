@@ -45,8 +45,8 @@
 #define PECH_MAIN_THREADS (64u * PECH_MAIN_WAVES)
 // Diagnostic switches that change results exist only with PECH_DIAG (A/B
 // builds, tools/build_ab.sh): a product build that sees one fails here.
-#if (defined(PECH_AB_NOLDS) || defined(PECH_AB_NOLOAD)) && !defined(PECH_DIAG)
-#error "PECH_AB_NOLDS / PECH_AB_NOLOAD produce wrong CRCs: diagnostic builds must also define PECH_DIAG"
+#if (defined(PECH_AB_NOLDS) || defined(PECH_AB_NOLOAD) || defined(PECH_AB_NOATOMIC)) && !defined(PECH_DIAG)
+#error "PECH_AB_NOLDS / PECH_AB_NOLOAD / PECH_AB_NOATOMIC produce wrong CRCs: diagnostic builds must also define PECH_DIAG"
 #endif
 
 // Split-step results are XORed into a workgroup table in LDS and reach out[]
@@ -782,6 +782,9 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 				atomicXor(out + o0, v);
 		}
 	} else if (active && g8 == 0) {
+#ifdef PECH_AB_NOATOMIC // diagnostic build only: run results of non-split steps dropped (wrong CRCs)
+		if (v == 0x9E3779B9u)
+#endif
 		atomicXor(out + orig, v);
 	}
 }
