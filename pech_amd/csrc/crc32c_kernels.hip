@@ -68,7 +68,8 @@
 #define L_DEFER (L_NZ + 4096u)   // 512 B: split-step results, keyed by output slot
 #define L_DEFER_DONE (L_DEFER + 8u * PECH_DEFER_SLOTS) // waves of the workgroup done
 #define L_XINV (L_DEFER_DONE + 16u) // 512 B: x^(-8k), k < 128
-#define L_BYTES (L_XINV + 512u)
+#define L_POOL (L_XINV + 512u)   // 16 B: the workgroup's next pooled item (uniform batches)
+#define L_BYTES (L_POOL + 16u)
 static_assert(L_BYTES <= 160u * 1024u, "main kernel LDS over 160 KiB");
 
 static_assert(L_POWB - L_TAB4 == 4u * (PECH_C_POWB - PECH_C_TAB4), "LDS/consts layout mismatch");
@@ -227,6 +228,7 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	__shared__ uint32_t wcnt[PECH_NCLASS * PECH_WAVES_PER_WG]; // per (class, wave): buffers, then their offset
 	__shared__ uint32_t rows_at[PECH_CHUNK];
 	__shared__ uint32_t scratch[PECH_WAVES_PER_WG];
+	__shared__ uint32_t rmax; // largest core of the chunk (uniformity flag)
 	const uint32_t tid = threadIdx.x;
 	const uint32_t b = blockIdx.x * PECH_CHUNK + tid;
 	// All three loads unconditional (clamped indices) so they are in flight
@@ -258,6 +260,8 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	if (tid < 384)
 		powb[tid] = tvp;
 	rows_at[tid] = 0;
+	if (tid == 0)
+		rmax = 0;
 	__syncthreads();
 
 	uint32_t rows = 0, cls = 0;
@@ -316,6 +320,14 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 		}
 		out[b] = res;
 	}
+	{ // the chunk's largest core: a wave max by lane swaps, then one LDS atomic per wave
+		uint32_t m = rows;
+#pragma unroll
+		for (uint32_t off = 32; off; off >>= 1)
+			m = max(m, (uint32_t)__shfl_xor((int)m, (int)off));
+		if ((tid & 63u) == 0 && m)
+			atomicMax(&rmax, m);
+	}
 	// Order the chunk's buffers by size class, STABLY (descriptor order inside
 	// a class): per-wave ballots, then one scan over (class, wave).
 	const uint32_t lane = tid & 63u, wave = tid >> 6;
@@ -329,14 +341,12 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 			wcnt[c * PECH_WAVES_PER_WG + wave] = (uint32_t)__builtin_popcountll(m);
 	}
 	__syncthreads();
+	uint32_t nz;
 	{
-		uint32_t nz;
 		const uint32_t v = tid < PECH_NCLASS * PECH_WAVES_PER_WG ? wcnt[tid] : 0u;
 		const uint32_t ex = block_excl_scan(v, scratch, &nz); // (barriers inside)
 		if (tid < PECH_NCLASS * PECH_WAVES_PER_WG)
 			wcnt[tid] = ex;
-		if (tid == 0)
-			nzs[blockIdx.x] = nz;
 		__syncthreads();
 		if (rows) {
 			// Inside every full block of 16 same-class buffers below the split
@@ -362,8 +372,15 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	uint32_t total;
 	const uint32_t ex = block_excl_scan(rows_at[tid], scratch, &total);
 	lrs[blockIdx.x * PECH_CHUNK + tid] = ex;
-	if (tid == 0)
+	if (tid == 0) {
 		partials[blockIdx.x] = total;
+		// uniform chunk: every buffer has a core and all cores have the
+		// largest one's rows (sum == count x max); the main kernel then
+		// locates any row by division and pools its work (PECH_ITEM_ROWS)
+		const uint32_t cnt = min(PECH_CHUNK, n - blockIdx.x * PECH_CHUNK);
+		const bool uni = nz == cnt && (uint64_t)nz * rmax == (uint64_t)total && total != 0;
+		nzs[blockIdx.x] = nz | (uni ? PECH_NZ_UNIFORM : 0u);
+	}
 }
 
 extern "C" __global__ __launch_bounds__(PECH_WG_THREADS) void pech_crc32c_plan(
@@ -812,6 +829,14 @@ __device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, b
 		__builtin_nontemporal_store(v, (g_u32x4w *)(S.dad + (uint64_t)row * PECH_ROW_BYTES));
 }
 
+// Uniform batches: the end of share [a, b)'s head, which its owner walks
+// first; the rest of the share (at most PECH_POOL_ROWS rows) is pooled.  The
+// head is at least one item, or the whole share.
+__device__ __forceinline__ uint32_t share_head(uint32_t a, uint32_t b)
+{
+	return min(b, max(a + PECH_ITEM_ROWS, b - min(PECH_POOL_ROWS, b - a)));
+}
+
 template <bool COPY, uint32_t U>
 __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
 					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
@@ -895,15 +920,28 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 
 	// the wave's own exclusive scan of the chunk totals
 	uint32_t pc[16], nc[16], lsum = 0;
+	bool uflag = true;
 #pragma unroll
 	for (uint32_t k = 0; k < 16; ++k) {
 		const bool real = lane * 16u + k < nchunks;
+		const uint32_t nzf = real ? nv4[k >> 2][k & 3u] : PECH_NZ_UNIFORM;
 		pc[k] = real ? pv4[k >> 2][k & 3u] : 0u;
-		nc[k] = real ? nv4[k >> 2][k & 3u] : 0u;
+		nc[k] = nzf & ~PECH_NZ_UNIFORM;
+		uflag = uflag && (nzf & PECH_NZ_UNIFORM) != 0u;
 		lsum += pc[k];
 	}
 	const uint32_t incl = wave_incl_scan(lsum);
 	const uint32_t Rtot = lane_value(incl, 63);
+	// Uniform batch (every chunk flagged by the plan kernel, all with chunk
+	// 0's rows per buffer): position p holds rows [p U0, (p+1) U0), so any row
+	// is located by a division, and the workgroup pools its rows in items.
+	const uint32_t nz0 = lane_value(nc[0], 0); // (lane values: wave-uniform, as the pool needs)
+	const uint32_t U0 = nz0 ? lane_value(pc[0], 0) / nz0 : 0u;
+	bool uok = uflag;
+#pragma unroll
+	for (uint32_t k = 0; k < 16; ++k)
+		uok = uok && (uint64_t)nc[k] * U0 == (uint64_t)pc[k];
+	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
 	STAMP(t_scan);
 	// Every wave gets an equal share of the batch's rows (at least rpw_min).
 	const uint32_t rpw_eq = Rtot ? (Rtot - 1u) / W + 1u : 0u;
@@ -918,7 +956,23 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t wg_rows = (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
 	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
 	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
-	const uint32_t rem_all = r1 - r0;
+	// Uniform batches: a wave starts on its share's head [r0, t) and then
+	// takes items of PECH_ITEM_ROWS rows from the workgroup's pool of share
+	// tails (at most PECH_POOL_ROWS of each share; an LDS counter, claim c is
+	// tail item c/16 of share c%16, located by division), so the CU's 16
+	// waves -- issued oldest-first, which made equal static shares finish up
+	// to 60 us apart -- end together, and the CU is free for the next
+	// launch's workgroup that much earlier.  (The fused copy keeps static
+	// shares: pooled items cost it 14 % per launch, profiles/r02/ab_item_pool.txt.)
+#ifdef PECH_NO_POOL // A/B: static shares for every batch
+	const uint32_t jmax = 0u;
+#else
+	const uint32_t jmax = !COPY && uniform ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
+										      PECH_MAIN_WAVES) + PECH_ITEM_ROWS - 1u) /
+							     PECH_ITEM_ROWS
+					       : 0u;
+#endif
+	const uint32_t rem_all = jmax ? share_head(r0, r1) - r0 : r1 - r0;
 
 	// nz table for plan_step: every wave writes all of it (the same values)
 	// and reads back only its own writes until the barrier below
@@ -1020,6 +1074,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
 	if (tid < 128u)
 		lds[L_XINV / 4u + tid] = txi;
+	if (tid == 0)
+		lds[L_POOL / 4u] = 0u;
 	if (tid < PECH_DEFER_SLOTS) {
 		lds[L_DEFER / 4u + tid] = PECH_DEFER_EMPTY;
 		lds[L_DEFER / 4u + PECH_DEFER_SLOTS + tid] = 0u;
@@ -1029,6 +1085,11 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	STAMP(t_fill);
 	__syncthreads(); // tables published; every wave's prime is already in flight
 	STAMP(t_start);
+	// the wave's first pool claim, one item ahead (resolved when its first
+	// item is done)
+	uint32_t claim = 0;
+	if (jmax > 1u && lane == 0)
+		claim = atomicAdd(lds + L_POOL / 4u, 1u);
 #ifdef PECH_STAMPS
 	uint64_t tq[3] = {0, 0, 0};
 	uint32_t nstep = 0;
@@ -1104,7 +1165,28 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// already fetch the next step's first rows
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
-		const Step N = plan_step<COPY>(cores, deltas, lds, S.pos, S.lr, S.rem, lane, g8, grp);
+		uint32_t npos = S.pos, nlr = S.lr, nrem = S.rem;
+		if (jmax > 1u && nrem == 0) {
+			// item done: the next one from the pool (wave-uniform branch,
+			// scalar work and an LDS atomic; the ring is untouched)
+			for (;;) {
+				const uint32_t c = uni(claim), j = 1u + (c >> 4), sh = c & 15u;
+				if (j >= jmax)
+					break; // pool empty
+				const uint32_t a = (uint32_t)(wg0 + (uint64_t)wg_rows * sh / PECH_MAIN_WAVES);
+				const uint32_t b = (uint32_t)(wg0 + (uint64_t)wg_rows * (sh + 1u) / PECH_MAIN_WAVES);
+				const uint32_t st = share_head(a, b) + (j - 1u) * PECH_ITEM_ROWS;
+				if (lane == 0)
+					claim = atomicAdd(lds + L_POOL / 4u, 1u); // the next claim, one item ahead
+				if (st < b) {
+					npos = st / U0;
+					nlr = st - npos * U0;
+					nrem = min(PECH_ITEM_ROWS, b - st);
+					break;
+				}
+			}
+		}
+		const Step N = plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp);
 		if constexpr (COPY) { // block discipline: this block's rows and stores, then the next step's loads
 			const bool more = N.T != 0;
 			const Step &L = more ? N : S;
@@ -1265,6 +1347,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.14 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
-		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY);
+	return "pech_crc32c 0.15 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS);
 }

@@ -41,6 +41,13 @@
 #define PECH_RPW_MIN 64u          /* min rows per wave (8 KiB)             */
 #define PECH_LARGE_ROWS 2048u     /* size-class cap for the plan's ordering  */
 #define PECH_SPLIT_ROWS 256u      /* >= this: a buffer is split over 8 groups */
+#ifndef PECH_ITEM_ROWS
+#define PECH_ITEM_ROWS 256u       /* uniform batches: rows per pooled work item */
+#endif
+#ifndef PECH_POOL_ROWS
+#define PECH_POOL_ROWS 512u       /* uniform batches: at most this many of a wave's rows are pooled */
+#endif
+#define PECH_NZ_UNIFORM 0x80000000u /* nzs[] flag: every buffer of the chunk has a core of the same rows */
 #define PECH_SMALL_MAX 65536u     /* drop-in crc32c(): one-launch path up to this */
 #define PECH_DROPIN_CPU_MAX_DEFAULT (4u << 20) /* drop-in crc32c(): host routine up to this */
 /* payload of one launch: rows (128 B) are counted in 32 bits, so < 512 GiB */
@@ -113,7 +120,7 @@ LAYOUT_FN uint32_t pech_size_class(uint32_t rows)
  *   cores    pech_core[slots]        sorted core descriptors per chunk
  *   lrs      u32[slots]              chunk-local exclusive row scan
  *   partials u32[PECH_MAX_CHUNKS]    rows per chunk
- *   nzs      u32[PECH_MAX_CHUNKS]    non-empty cores per chunk
+ *   nzs      u32[PECH_MAX_CHUNKS]    non-empty cores per chunk | PECH_NZ_UNIFORM
  *   deltas   i64[slots]              fused copy: destination - source per buffer
  * slots = nch * PECH_CHUNK, nch = ceil(m / PECH_CHUNK). */
 struct pech_ws {

@@ -35,6 +35,15 @@ CHUNK = C["PECH_CHUNK"]
 SPLIT = C["PECH_SPLIT_ROWS"]
 LARGE = C["PECH_LARGE_ROWS"]
 WAVES_PER_WG = C["PECH_MAIN_WAVES"]
+ITEM = C["PECH_ITEM_ROWS"]
+POOL = C.get("PECH_POOL_ROWS", 0xFFFFFFFF)
+
+
+def share_head(a, b, item=None, pool=None):
+    """kernel share_head: end of the head of share [a, b) its owner walks first"""
+    item, pool = item or ITEM, pool or POOL
+    return min(b, max(a + item, b - min(pool, b - a)))
+NZ_UNIFORM = 0x80000000
 
 
 def core_rows(addr, ln):
@@ -101,7 +110,12 @@ def plan(descs, rng=None):
                 cores[c * CHUNK + pos] = order[pos]
                 acc += order[pos]["rows"]
         partials.append(acc)
-        nzs.append(len(order))
+        # uniform chunk (plan kernel): every buffer has a core, all of the
+        # largest one's rows -> flag bit in nzs
+        cnt = min(n, (c + 1) * CHUNK) - c * CHUNK
+        rmax = max((it["rows"] for it in order), default=0)
+        uni = len(order) == cnt and len(order) * rmax == acc and acc != 0
+        nzs.append(len(order) | (NZ_UNIFORM if uni else 0))
     return cores, lrs, partials, nzs
 
 
@@ -160,6 +174,7 @@ def find_start(lrs, pref, nzs, r):
     """find_start_wave: chunk by binary search of the prefix, then the count
     of the chunk's row offsets <= the chunk-local row (one wave-wide read of
     all PECH_CHUNK offsets, entries past nz excluded)."""
+    nzs = [z & ~NZ_UNIFORM for z in nzs]
     nchunks = len(nzs)
     clo, chi = 0, nchunks
     while chi - clo > 1:
@@ -209,15 +224,37 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
         pref.append(pref[-1] + p)
     Rtot = pref[-1]
     events = []
-    for r0, r1 in wave_ranges(Rtot, ncu, rpw_min, weights):
-        if r1 > r0:
-            pos, lr = find_start(lrs, pref, nzs, r0)
-            walk(cores, nzs, pos, lr, r1 - r0, U, events)
+    # uniform batch (kernel prologue): every chunk flagged, all with chunk 0's
+    # rows per buffer -> items of ITEM rows: each wave's share's first item by
+    # its owner, the rest from the workgroup pool (claim c: item 1 + c//16 of
+    # share c%16; which wave takes a claim does not matter for coverage)
+    nz = [z & ~NZ_UNIFORM for z in nzs]
+    U0 = partials[0] // nz[0] if nz and nz[0] else 0
+    uniform = bool(U0) and all((z & NZ_UNIFORM) and n * U0 == p for z, n, p in zip(nzs, nz, partials))
+    ranges = wave_ranges(Rtot, ncu, rpw_min, weights)
+    for w0 in range(0, len(ranges), WAVES_PER_WG):
+        shares = ranges[w0:w0 + WAVES_PER_WG]
+        wg_rows = shares[-1][1] - shares[0][0]
+        jmax = 1 + (min(POOL, (wg_rows + WAVES_PER_WG - 1) // WAVES_PER_WG) + ITEM - 1) // ITEM if uniform else 0
+        for r0, r1 in shares:
+            if r1 > r0:
+                pos, lr = find_start(lrs, pref, nzs, r0)
+                walk(cores, nzs, pos, lr, share_head(r0, r1) - r0 if jmax else r1 - r0, U, events)
+        if jmax > 1:
+            for c in range(WAVES_PER_WG * (jmax - 1)):
+                j, sh = 1 + c // WAVES_PER_WG, c % WAVES_PER_WG
+                a, b = shares[sh]
+                st = share_head(a, b) + (j - 1) * ITEM
+                if st < b:
+                    pos, lr = st // U0, st % U0
+                    assert (pos, lr) == find_start(lrs, pref, nzs, st), (st, pos, lr)
+                    walk(cores, nzs, pos, lr, min(ITEM, b - st), U, events)
     return events
 
 
 def walk(cores, nzs, pos, lr, rem, U, events):
     """plan_step + run of one sub-range (pos, lr, rem)."""
+    nzs = [z & ~NZ_UNIFORM for z in nzs]
     if True:
         guard = 0
         while rem:

@@ -52,6 +52,28 @@ def test_uniform_4m_like():
     check([(0x100000 * (i + 1), 300000) for i in range(6)], ncu=2)
 
 
+def test_uniform_pool_4k_many_chunks():
+    # uniform batch over 3 chunks (the last partial): items of PECH_ITEM_ROWS
+    # from the workgroup pool, each located by division (checked against the
+    # row-offset search inside the model)
+    descs = [(0x10000 + 4096 * i, 4096) for i in range(2500)]
+    cores, lrs, partials, nzs = KM.plan(descs)
+    assert all(z & KM.NZ_UNIFORM for z in nzs)
+    check(descs, ncu=2)
+
+
+def test_uniform_pool_large_buffers():
+    check([(0x100000 * (i + 1), 1 << 20) for i in range(5)], ncu=1)
+
+
+def test_not_uniform_when_chunks_differ():
+    # each chunk uniform on its own, different rows per buffer: static shares
+    descs = [(0x10000 + 8192 * i, 4096 if i < 1024 else 8192) for i in range(2048)]
+    cores, lrs, partials, nzs = KM.plan(descs)
+    assert all(z & KM.NZ_UNIFORM for z in nzs) and partials[0] // 1024 != partials[1] // 1024
+    check(descs, ncu=1)
+
+
 def test_tiny_and_unaligned():
     rng = random.Random(1)
     descs = []
@@ -108,3 +130,12 @@ def test_wave_ranges_partition_row_space(Rtot, ncu):
         assert r0 == pos and r1 >= r0
         pos = r1
     assert pos == Rtot
+
+
+@pytest.mark.parametrize("item,pool", [(64, 200), (256, 1024), (512, 0xFFFFFFFF), (32, 32)])
+def test_pool_item_and_tail_sizes(monkeypatch, item, pool):
+    # the A/B sizes of the pooled share tails: every row still consumed once
+    monkeypatch.setattr(KM, "ITEM", item)
+    monkeypatch.setattr(KM, "POOL", pool)
+    check([(0x10000 + 4096 * i, 4096) for i in range(1500)], ncu=1)
+    check([(0x100000 * (i + 1), 1 << 20) for i in range(3)], ncu=1)

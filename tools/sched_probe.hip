@@ -24,6 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <vector>
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1014,6 +1015,50 @@ int main(int argc, char **argv)
 			printf("%s  {\"probe\": \"static + %u extra WGs over the last %.1f%% (idle %u us)\", \"us\": %.2f, \"GBps\": %.1f}",
 			       sep(), ex[v].X, ex[v].permille / 10.0, ex[v].idle, tot / reps * 1e3, bytes / (tot / reps * 1e-3) / 1e9);
 		}
+	}
+	if (!strcmp(which, "pipe")) {
+		// Pipelined rate: 40 launches alternating over two streams (the bench's
+		// `value` pass), each persistent launch holding 144 KiB of LDS per
+		// workgroup as the CRC kernel does (one workgroup per CU), so a CU takes
+		// the next launch's workgroup only once all 16 waves of the current one
+		// have exited.  Static shares vs the intra-workgroup pool (waves of a CU
+		// finish together), and the grid for reference.
+		hipStream_t st[2];
+		CHECK(hipStreamCreateWithFlags(&st[0], hipStreamNonBlocking));
+		CHECK(hipStreamCreateWithFlags(&st[1], hipStreamNonBlocking));
+		const size_t lds = 144u * 1024u;
+		CHECK(hipFuncSetAttribute((const void *)k_sched<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		CHECK(hipFuncSetAttribute((const void *)k_wgpool, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		const char *names[] = {"pipe static", "pipe wgpool S512", "pipe wgpool S256", "pipe grid float4 nt",
+				       "serial static", "serial wgpool S512"};
+		const int nl = 40;
+		for (int pass = 0; pass < 2; ++pass)
+			for (int v = 0; v < 6; ++v) {
+				double best = 1e30;
+				for (int rep = 0; rep < 3; ++rep) {
+					CHECK(hipDeviceSynchronize());
+					const auto t0 = std::chrono::steady_clock::now();
+					for (int i = 0; i < nl; ++i) {
+						hipStream_t s = v >= 4 ? st[0] : st[i & 1];
+						const uint8_t *src = buf[i & 1];
+						if (v == 0 || v == 4)
+							hipLaunchKernelGGL(k_sched<0>, dim3(ncu), dim3(1024), lds, s, src, R, ctl, 0u, out, nsteal);
+						else if (v == 1 || v == 5)
+							hipLaunchKernelGGL(k_wgpool, dim3(ncu), dim3(1024), lds, s, src, R, 512u, out);
+						else if (v == 2)
+							hipLaunchKernelGGL(k_wgpool, dim3(ncu), dim3(1024), lds, s, src, R, 256u, out);
+						else
+							hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(bytes / 16 / 256)), dim3(256), 0, s,
+									   src, (uint64_t)(bytes / 16), out);
+					}
+					CHECK(hipDeviceSynchronize());
+					const double us =
+						std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / nl;
+					best = us < best ? us : best;
+				}
+				printf("%s  {\"probe\": \"%s\", \"us_per_launch\": %.2f, \"GBps\": %.1f}", sep(), names[v], best,
+				       bytes / (best * 1e-6) / 1e9);
+			}
 	}
 	if (!strcmp(which, "wide")) { // group-sliced static vs row-interleaved static vs the grid, two passes
 		const char *names[] = {"read static (group slices)", "read static wide D8 (rows interleaved over groups)",
