@@ -963,7 +963,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// waves -- issued oldest-first, which made equal static shares finish up
 	// to 60 us apart -- end together, and the CU is free for the next
 	// launch's workgroup that much earlier.  (The fused copy keeps static
-	// shares: pooled items cost it 14 % per launch, profiles/r02/ab_item_pool.txt.)
+	// shares: pooled items cost it 9-14 % per launch, profiles/r02/ab_item_pool.txt.)
 #ifdef PECH_NO_POOL // A/B: static shares for every batch
 	const uint32_t jmax = 0u;
 #else
