@@ -13,7 +13,7 @@ HOST_OBJ = build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o build/crc3
 OBJ = build/crc32c_kernels.o $(HOST_OBJ)
 
 all: $(LIB) oracle build/msgr_sim build/msgr_conn_sim build/dropin_kat build/coro_stack build/dropin_bench \
-     build/lib_dbg.so build/hbm_probe build/sched_probe
+     build/lib_dbg.so build/lib_test.so build/hbm_probe build/sched_probe
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -56,6 +56,21 @@ variant: $(HOST_OBJ)
 build/lib_dbg.so: pech_amd/csrc/crc32c_kernels.hip $(HDR) $(HOST_OBJ)
 	$(HIPCC) $(HIPFLAGS) -DPECH_DEBUG_BOUNDS -c pech_amd/csrc/crc32c_kernels.hip -o build/k_dbg.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/k_dbg.o $(HOST_OBJ)
+
+# test build for the failure-path tests (tests/test_faults.py): the same objects,
+# except that crc32c_api is compiled with the fault-injection hook
+# (crc32c_test_inject), which the release library does not have
+build/crc32c_api_test.o: pech_amd/csrc/crc32c_api.cpp $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DPECH_TEST_HOOKS -x hip -c $< -o $@
+
+build/crc32c_async_test.o: pech_amd/csrc/crc32c_async.cpp $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DPECH_TEST_HOOKS -x hip -c $< -o $@
+
+build/lib_test.so: build/crc32c_kernels.o build/crc32c_api_test.o build/crc32c_async_test.o build/crc32c_cpu.o \
+		   build/crc32c_msgr.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 # test program: pech's receive path on the async layer (gnu89, epoll loop);
 # links the test oracle for the expected footer CRCs -- not product code

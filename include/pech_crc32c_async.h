@@ -102,7 +102,11 @@ int crc32c_async_flush(struct crc32c_async *a);
 
 /* Run the callbacks of every finished batch, in submission order, on the
  * calling thread; clears the eventfd.  Returns the number of callbacks run
- * (>= 0) or a negative errno.  Never blocks. */
+ * (>= 0) or a negative errno.  Never blocks.  A batch whose stream failed
+ * after the launch never signals the eventfd (HIP skips its host function);
+ * complete() finds it by querying the stream and fails its payloads (err
+ * -EIO).  So the loop calls complete() when the fd fires AND from a timer
+ * (pech: a timer_list of a few ms) while crc32c_async_pending() > 0. */
 int crc32c_async_complete(struct crc32c_async *a);
 
 /* Flush and wait until every submission's callback has run (shutdown, tests). */

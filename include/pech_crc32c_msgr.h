@@ -41,7 +41,8 @@
  * batch is recomputed on the host from the same bytes.
  * Threading: as the async layer -- one caller thread; the kick and release
  * callbacks run inside crc32c_async_complete() on that thread (release also
- * inside reset / destroy).
+ * inside reset / cancel / destroy).  The adapter keeps no locks: its
+ * connections and counters belong to that thread.
  * Errors: 0 / negative errno (include/err.h style).
  */
 #ifndef PECH_CRC32C_MSGR_H
@@ -71,20 +72,31 @@ struct crc32c_msgr_conn *crc32c_msgr_conn_create(struct crc32c_async *a, unsigne
 						 crc32c_msgr_kick_fn kick, void *kick_arg,
 						 crc32c_msgr_release_fn release);
 
-/* Fault / reconnect (con_fault, reset_connection): every queued receive
- * message is released (now, or when its in-flight CRC completes); send
- * entries are kept (a resent message reuses its CRC: the bytes are the same). */
+/* Fault / reconnect (con_fault): every queued receive message is released
+ * (now, or when its in-flight CRC completes); send entries are kept (a
+ * resent message reuses its CRC: the bytes are the same). */
 void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c);
 
-/* Reset, release the send entries too, free the adapter. */
+/* Reset, release the send entries too (crc32c_msgr_tx_cancel(c, NULL)),
+ * free the adapter. */
 void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c);
+
+/* Payloads of at most `bytes` (default 16 KiB, or PECH_CRC32C_MSGR_HOST_MAX
+ * in the environment) are checksummed at once on the host instead of the
+ * GPU: below the crossover the host routine costs less CPU time than the
+ * GPU round trip.  Process-wide; returns the previous
+ * value.  0 sends every checked payload to the GPU. */
+unsigned int crc32c_msgr_set_host_max(unsigned int bytes);
 
 /* RECEIVE, at the footer (read_partial_message :2816): queue msg, whose data
  * section is data[0, len).  check != 0 (do_datacrc and the footer has no
- * CEPH_MSG_FOOTER_NOCRC flag): crc32c(0, data, len) is computed on the GPU
- * and compared with footer_crc; otherwise the message is ready at once.  The
- * messenger must not modify or free data until msg is returned by rx_next or
- * released.  0, -EAGAIN (queue full: stop reading, dispatch first), or < 0. */
+ * CEPH_MSG_FOOTER_NOCRC flag): crc32c(0, data, len) is computed (on the GPU,
+ * or on the host up to crc32c_msgr_set_host_max()) and compared with
+ * footer_crc; otherwise the message is ready at once.  msg may be NULL with
+ * check == 0: an in-order marker for a message the messenger skipped, so
+ * in_seq still advances in arrival order.  The messenger must not modify or
+ * free data until msg is returned by rx_next or released.  0, -EAGAIN
+ * (queue full: stop reading, dispatch first), or < 0. */
 int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data, unsigned int len, int check,
 			 uint32_t footer_crc);
 
@@ -101,13 +113,26 @@ int crc32c_msgr_rx_next(struct crc32c_msgr_conn *c, void **msg, uint32_t *crc);
 unsigned int crc32c_msgr_rx_pending(const struct crc32c_msgr_conn *c);
 
 /* SEND: submit crc32c(seed, data, len) of outgoing msg (prepare_write_message;
- * seed = footer.data_crc, 0 for a new message).  A msg that already has an
- * entry (resend after a fault) keeps it: 0 without new work. */
+ * seed = footer.data_crc, 0 for a new message).  0: a new entry (the adapter
+ * now holds the caller's reference to msg, returned by tx_footer or
+ * release); 1: msg already has an entry (resend after a fault, or
+ * tx_known): nothing new is taken; < 0 error. */
 int crc32c_msgr_tx_submit(struct crc32c_msgr_conn *c, void *msg, const void *data, unsigned int len, uint32_t seed);
 
 /* SEND without a data pass: msg's data CRC is already known (REPOP fan-out:
- * the verified request CRC, or crc32c_concat() of segment CRCs). */
+ * the verified request CRC, or crc32c_concat() of segment CRCs).  Returns
+ * as tx_submit. */
 int crc32c_msgr_tx_known(struct crc32c_msgr_conn *c, void *msg, uint32_t crc);
+
+/* 1 if msg has a send entry (submitted or known), else 0. */
+int crc32c_msgr_tx_has(const struct crc32c_msgr_conn *c, const void *msg);
+
+/* Drop msg's send entry (msg NULL: every send entry of c), for messages the
+ * messenger discards unsent: reset_connection drops out_queue/out_sent
+ * (messenger.c:724-731), ceph_msg_revoke (:3749).  Each dropped entry's
+ * reference comes back through release(): now, or when its in-flight CRC
+ * lands.  Returns the number of entries dropped. */
+unsigned int crc32c_msgr_tx_cancel(struct crc32c_msgr_conn *c, void *msg);
 
 /* At the end of msg's data (write_partial_message_data :1793): 1 and *crc
  * when ready (the entry is consumed), 0 when still running (hold the footer:
@@ -118,6 +143,7 @@ int crc32c_msgr_tx_footer(struct crc32c_msgr_conn *c, void *msg, uint32_t *crc);
 struct crc32c_msgr_stats {
 	uint64_t rx_submitted, rx_unchecked, rx_verified, rx_bad, rx_released;
 	uint64_t tx_submitted, tx_known, tx_held, tx_released; /* held: footers that had to wait */
+	uint64_t rx_host, tx_host; /* checksummed on the host: small payloads, refused submissions */
 };
 void crc32c_msgr_get_stats(struct crc32c_msgr_stats *st);
 

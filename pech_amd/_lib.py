@@ -89,7 +89,17 @@ SIGNATURES = {
     "crc32c_msgr_tx_known": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "crc32c_msgr_tx_footer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "crc32c_msgr_get_stats": (None, [ctypes.c_void_p]),
+    "crc32c_msgr_set_host_max": (ctypes.c_uint, [ctypes.c_uint]),
+    "crc32c_msgr_tx_has": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "crc32c_msgr_tx_cancel": (ctypes.c_uint, [ctypes.c_void_p, ctypes.c_void_p]),
 }
+
+
+class CMsgrStats(ctypes.Structure):
+    """struct crc32c_msgr_stats (include/pech_crc32c_msgr.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("rx_submitted", "rx_unchecked", "rx_verified", "rx_bad",
+                                                "rx_released", "tx_submitted", "tx_known", "tx_held",
+                                                "tx_released", "rx_host", "tx_host")]
 
 
 def lib():

@@ -247,12 +247,20 @@ class AsyncCrc:
             raise Crc32cError(f"crc32c_async_create failed: {lib().crc32c_last_error().decode()}")
         self._keep = {}  # submission key -> (payload ref, python callback)
         self._next = 0
+        self.stray = 0  # callbacks for submissions that returned an error (must stay 0)
 
         def trampoline(arg, crc, err):
-            ref, cb = self._keep.pop(arg)
-            cb(crc, err)
+            ent = self._keep.pop(arg, None)
+            if ent is None:
+                self.stray += 1
+                return
+            ent[1](crc, err)
 
         self._cfn = DONE_FN(trampoline)
+
+    @property
+    def handle(self):
+        return self._h
 
     def fd(self):
         return lib().crc32c_async_fd(self._h)

@@ -48,7 +48,8 @@ enum pech_fault_site {
 	PECH_FAULT_DROPIN_GPU = 0, // drop-in crc32c(): its GPU launch fails
 	PECH_FAULT_ASYNC_LAUNCH = 1, // async: a slot's kernel launch fails
 	PECH_FAULT_ASYNC_DMA = 2,    // async: a payload's H2D DMA fails
-	PECH_FAULT_SITES = 3
+	PECH_FAULT_ASYNC_STREAM = 3, // async: a launched batch's stream fails (no host function, query error)
+	PECH_FAULT_SITES = 4
 };
 PECH_HIDDEN bool pech_fault(int site);
 

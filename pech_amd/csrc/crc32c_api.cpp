@@ -753,6 +753,10 @@ static std::atomic<int> g_fault[PECH_FAULT_SITES];
 
 PECH_HIDDEN bool pech_fault(int site)
 {
+#ifndef PECH_TEST_HOOKS
+	(void)site;
+	return false; // release build: nothing can arm a fault
+#endif
 	if (site < 0 || site >= PECH_FAULT_SITES)
 		return false;
 	int v = g_fault[site].load(std::memory_order_relaxed);
@@ -1074,8 +1078,10 @@ const char *crc32c_version(void)
 	return pech_kernel_tag();
 }
 
-// ---- test hooks (tests/test_cpu_path.py, tests/test_faults.py); not in
-// include/: they exercise paths a healthy GPU never takes
+// ---- test hooks; not in include/.  Failure injection exists only in the
+// test build (build/lib_test.so, -DPECH_TEST_HOOKS, tests/test_faults.py):
+// the release library cannot be made to fail on purpose.
+#ifdef PECH_TEST_HOOKS
 // arm fault `site` (enum pech_fault_site) to fire on its countdown-th use
 int crc32c_test_inject(int site, int countdown)
 {
@@ -1084,7 +1090,9 @@ int crc32c_test_inject(int site, int countdown)
 	g_fault[site].store(countdown);
 	return 0;
 }
+#endif
 
+// Read-only diagnostics (tests/test_cpu_path.py): they change no state.
 // the host routine itself: variant 0 = the one crc32c() uses (SSE4.2 when
 // the CPU has it), 1 = portable slice-by-8
 uint32_t crc32c_test_cpu(uint32_t crc, const void *data, size_t n, int variant)

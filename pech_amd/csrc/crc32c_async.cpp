@@ -26,7 +26,12 @@
 // Failures: a failed H2D, launch or batch fails every payload with a piece
 // in that slot (callback err = -EIO), makes the context's error sticky and
 // bumps the eventfd so the loop collects them.  A submission that returns
-// an error never gets a callback.
+// an error never gets a callback -- also when its own submit filled the slot
+// and that launch failed.  A batch that fails after its launch (the stream
+// reports an error, so its host function never runs and the eventfd stays
+// quiet) is found by the next complete() or drain(), which ask the stream:
+// an epoll loop calls complete() when the fd fires AND from a timer while
+// crc32c_async_pending() > 0 (include/pech_crc32c_async.h).
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -226,6 +231,7 @@ struct Slot {
 	std::vector<std::pair<size_t, size_t>> packed; // staging runs filled by memcpy: [lo, hi)
 	size_t used = 0;
 	bool inflight = false;
+	bool inject_fail = false; // test build: this batch's stream "failed" (PECH_FAULT_ASYNC_STREAM)
 };
 
 struct Item {
@@ -331,6 +337,7 @@ static void harvest(crc32c_async *a, Slot *s, int err)
 	s->packed.clear();
 	s->used = 0;
 	s->inflight = false;
+	s->inject_fail = false;
 }
 
 // Harvest finished slots (blocking on the oldest when `wait`), in order.
@@ -341,12 +348,16 @@ static int reap(crc32c_async *a, bool wait_oldest)
 		hipError_t q = hipSuccess;
 		if (wait_oldest) {
 			q = hipStreamSynchronize(s->stream);
+			if (q == hipSuccess && s->inject_fail)
+				q = hipErrorLaunchFailure; // test build: as a failed stream reports itself
 			while (q == hipSuccess && !s->finished.load(std::memory_order_acquire)) {
 				// the host function runs on the runtime's thread: a moment
 			}
 		} else if (!s->finished.load(std::memory_order_acquire)) {
 			// a failed stream never runs its host function: ask the stream
 			q = hipStreamQuery(s->stream);
+			if (q == hipSuccess && s->inject_fail)
+				q = hipErrorLaunchFailure; // test build: as a failed stream reports itself
 			if (q == hipSuccess || q == hipErrorNotReady) {
 				(void)hipGetLastError();
 				return 0;
@@ -434,7 +445,11 @@ static int launch_slot(crc32c_async *a)
 	if (rc)
 		return fail_cur_slot(a, rc);
 	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), fail_cur_slot(a, -EIO));
-	TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_cur_slot(a, -EIO));
+	// test build: a batch whose stream fails after the launch -- HIP then
+	// skips its host function, so the eventfd stays quiet
+	s->inject_fail = pech_fault(PECH_FAULT_ASYNC_STREAM);
+	if (!s->inject_fail)
+		TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_cur_slot(a, -EIO));
 	s->inflight = true;
 	a->inflight.push_back(s);
 	a->cur = nullptr;
@@ -556,8 +571,16 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 	it.placed = true;
 	it.total = placed;
 	Slot *s = a->cur;
-	if (s && (s->pieces.size() == kSlotDescs || s->used >= kSlotBytes))
-		return launch_slot(a); // a failure here fails this payload through its callback
+	if (s && (s->pieces.size() == kSlotDescs || s->used >= kSlotBytes)) {
+		const int rc = launch_slot(a);
+		// This payload filled the slot and its launch failed: its pieces are
+		// harvested with the error, but the submission returns it, so the
+		// item is retired without a callback (error return and callback are
+		// exclusive; the caller still owns the bytes and recomputes).
+		if (rc)
+			a->items[id - a->base].cancelled = true;
+		return rc;
+	}
 	return 0;
 }
 

@@ -3,12 +3,24 @@
  * per-connection receive verify queues and send-side deferred footers on top
  * of the async layer.  Plain C (gcc); the GPU work is the async layer's.
  *
+ * Routing by size: a payload of at most crc32c_msgr_set_host_max() bytes
+ * (default PECH_MSGR_HOST_MAX_DEFAULT) is checksummed at once on the host
+ * (pech_cpu_crc32c, crc32c_cpu.c, SSE4.2): below that size the host routine
+ * costs less CPU time than submitting, launching and completing the payload
+ * through the GPU (measured).  The entry is then ready at
+ * once and takes the same queue/footer path as a GPU payload, so the
+ * messenger's sequencing does not depend on the route.
+ *
  * A GPU failure never reaches the messenger as a wrong or missing CRC: a
  * submission the async layer refuses, or a batch that fails, is recomputed
- * on the host (pech_cpu_crc32c, crc32c_cpu.c) from the same bytes, which the
- * adapter still owns at that point.
+ * on the host from the same bytes, which the adapter still owns at that point.
+ *
+ * Single-threaded by contract (pech runs one OS thread, README:11-16): the
+ * connection state and the process-wide counters are plain data, touched only
+ * by the caller's thread (callbacks run inside crc32c_async_complete()).
  */
 #include <errno.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -16,6 +28,9 @@
 
 #define PECH_HIDDEN __attribute__((visibility("hidden")))
 PECH_HIDDEN uint32_t pech_cpu_crc32c(uint32_t crc, const void *data, size_t n);
+
+#define PECH_MSGR_HOST_MAX_DEFAULT (16u << 10)
+#define TX_BUCKETS 64u /* per connection, chained by msg address */
 
 enum { ST_WAIT, ST_DONE };
 
@@ -31,8 +46,10 @@ struct rx_ent {
 };
 
 struct tx_ent {
-	struct tx_ent *next;
-	struct crc32c_msgr_conn *conn; /* NULL: orphaned by destroy, released when its CRC lands */
+	struct tx_ent *next;  /* send order */
+	struct tx_ent **prev; /* the link that points here (send-order list) */
+	struct tx_ent *hnext; /* hash chain */
+	struct crc32c_msgr_conn *conn; /* NULL: orphaned (cancel/destroy), released when its CRC lands */
 	crc32c_msgr_release_fn release;
 	void *msg;
 	const void *data;
@@ -45,13 +62,39 @@ struct crc32c_msgr_conn {
 	struct crc32c_async *a;
 	unsigned int max_pending, npending;
 	struct rx_ent *head, *tail;
-	struct tx_ent *tx;
+	struct tx_ent *tx, **tx_tail; /* send order */
+	struct tx_ent *tx_hash[TX_BUCKETS];
 	crc32c_msgr_kick_fn kick;
 	void *kick_arg;
 	crc32c_msgr_release_fn release;
 };
 
 static struct crc32c_msgr_stats g_st;
+static unsigned int g_host_max = PECH_MSGR_HOST_MAX_DEFAULT;
+static int g_host_max_env;
+
+static unsigned int host_max(void)
+{
+	if (!g_host_max_env) {
+		const char *e = getenv("PECH_CRC32C_MSGR_HOST_MAX");
+		g_host_max_env = 1;
+		if (e && *e) {
+			char *end = NULL;
+			const unsigned long long v = strtoull(e, &end, 0);
+			if (end != e)
+				g_host_max = v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (unsigned int)v;
+		}
+	}
+	return g_host_max;
+}
+
+unsigned int crc32c_msgr_set_host_max(unsigned int bytes)
+{
+	const unsigned int prev = host_max();
+
+	g_host_max = bytes;
+	return prev;
+}
 
 static void kick(struct crc32c_msgr_conn *c)
 {
@@ -68,7 +111,8 @@ static void rx_done(void *arg, uint32_t crc, int err)
 	if (err) /* the GPU failed: same bytes, host routine */
 		crc = pech_cpu_crc32c(0, e->data, e->len);
 	if (!e->conn) {
-		e->release(e->msg);
+		if (e->msg)
+			e->release(e->msg);
 		g_st.rx_released++;
 		free(e);
 		return;
@@ -94,6 +138,7 @@ struct crc32c_msgr_conn *crc32c_msgr_conn_create(struct crc32c_async *a, unsigne
 	c->kick = kick_fn;
 	c->kick_arg = kick_arg;
 	c->release = release;
+	c->tx_tail = &c->tx;
 	return c;
 }
 
@@ -102,9 +147,9 @@ int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data
 {
 	struct rx_ent *e;
 
-	if (!c || (len && !data))
+	if (!c || (len && !data) || (!msg && check))
 		return -EINVAL;
-	if (c->npending >= c->max_pending)
+	if (c->npending >= c->max_pending && msg) /* skip markers hold no message: always taken */
 		return -EAGAIN;
 	e = calloc(1, sizeof(*e));
 	if (!e)
@@ -127,9 +172,16 @@ int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data
 		g_st.rx_unchecked++;
 		return 0;
 	}
+	if (host_max() && len <= host_max()) { /* small payload: the host routine is cheaper than a GPU round trip */
+		g_st.rx_host++;
+		e->got = pech_cpu_crc32c(0, data, len);
+		e->state = ST_DONE;
+		return 0;
+	}
 	g_st.rx_submitted++;
 	if (crc32c_async_submit(c->a, data, len, 0, rx_done, e)) {
-		/* refused (context error or no GPU): host routine now */
+		/* refused (context error or no GPU): no callback will come; host routine now */
+		g_st.rx_host++;
 		e->got = pech_cpu_crc32c(0, data, len);
 		e->state = ST_DONE;
 	}
@@ -168,28 +220,61 @@ unsigned int crc32c_msgr_rx_pending(const struct crc32c_msgr_conn *c)
 	return c ? c->npending : 0u;
 }
 
-void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c)
-{
-	struct rx_ent *e, *n;
+/* ---- send ------------------------------------------------------------- */
 
-	if (!c)
-		return;
-	for (e = c->head; e; e = n) {
-		n = e->next;
-		if (e->state == ST_WAIT) {
-			e->conn = NULL; /* the GPU still reads its bytes: released in rx_done */
-			e->next = NULL;
-		} else {
-			c->release(e->msg);
-			g_st.rx_released++;
-			free(e);
-		}
-	}
-	c->head = c->tail = NULL;
-	c->npending = 0;
+static unsigned int tx_bucket(const void *msg)
+{
+	uintptr_t h = (uintptr_t)msg;
+
+	h ^= h >> 17; /* messages are heap objects: drop the alignment bits */
+	h *= 0x9E3779B97F4A7C15ull;
+	return (unsigned int)(h >> 58) & (TX_BUCKETS - 1u);
 }
 
-/* ---- send ------------------------------------------------------------- */
+static struct tx_ent *tx_find(struct crc32c_msgr_conn *c, const void *msg)
+{
+	struct tx_ent *e;
+
+	for (e = c->tx_hash[tx_bucket(msg)]; e; e = e->hnext)
+		if (e->msg == msg)
+			return e;
+	return NULL;
+}
+
+/* take e off both of its connection's lists */
+static void tx_unlink(struct crc32c_msgr_conn *c, struct tx_ent *e)
+{
+	struct tx_ent **pp;
+
+	for (pp = &c->tx_hash[tx_bucket(e->msg)]; *pp != e; pp = &(*pp)->hnext)
+		;
+	*pp = e->hnext;
+	*e->prev = e->next;
+	if (e->next)
+		e->next->prev = e->prev;
+	else
+		c->tx_tail = e->prev;
+	e->next = e->hnext = NULL;
+	e->prev = NULL;
+}
+
+static struct tx_ent *tx_new(struct crc32c_msgr_conn *c, void *msg)
+{
+	struct tx_ent *e = calloc(1, sizeof(*e));
+	const unsigned int b = tx_bucket(msg);
+
+	if (!e)
+		return NULL;
+	e->conn = c;
+	e->release = c->release;
+	e->msg = msg;
+	e->prev = c->tx_tail; /* append: send order */
+	*c->tx_tail = e;
+	c->tx_tail = &e->next;
+	e->hnext = c->tx_hash[b];
+	c->tx_hash[b] = e;
+	return e;
+}
 
 static void tx_done(void *arg, uint32_t crc, int err)
 {
@@ -209,42 +294,14 @@ static void tx_done(void *arg, uint32_t crc, int err)
 		kick(e->conn);
 }
 
-static struct tx_ent *tx_find(struct crc32c_msgr_conn *c, void *msg, struct tx_ent ***link)
-{
-	struct tx_ent **pp;
-
-	for (pp = &c->tx; *pp; pp = &(*pp)->next)
-		if ((*pp)->msg == msg) {
-			if (link)
-				*link = pp;
-			return *pp;
-		}
-	return NULL;
-}
-
-static struct tx_ent *tx_new(struct crc32c_msgr_conn *c, void *msg)
-{
-	struct tx_ent *e = calloc(1, sizeof(*e)), **pp;
-
-	if (!e)
-		return NULL;
-	e->conn = c;
-	e->release = c->release;
-	e->msg = msg;
-	for (pp = &c->tx; *pp; pp = &(*pp)->next) /* send order */
-		;
-	*pp = e;
-	return e;
-}
-
 int crc32c_msgr_tx_submit(struct crc32c_msgr_conn *c, void *msg, const void *data, unsigned int len, uint32_t seed)
 {
 	struct tx_ent *e;
 
 	if (!c || (len && !data))
 		return -EINVAL;
-	if (tx_find(c, msg, NULL))
-		return 0; /* resend: the bytes and so the CRC are unchanged */
+	if (tx_find(c, msg))
+		return 1; /* resend: the bytes and so the CRC are unchanged; no new reference taken */
 	e = tx_new(c, msg);
 	if (!e)
 		return -ENOMEM;
@@ -252,8 +309,16 @@ int crc32c_msgr_tx_submit(struct crc32c_msgr_conn *c, void *msg, const void *dat
 	e->len = len;
 	e->seed = seed;
 	e->state = ST_WAIT;
+	if (host_max() && len <= host_max()) {
+		g_st.tx_host++;
+		e->crc = pech_cpu_crc32c(seed, data, len);
+		e->state = ST_DONE;
+		return 0;
+	}
 	g_st.tx_submitted++;
 	if (crc32c_async_submit(c->a, data, len, seed, tx_done, e)) {
+		/* refused: no callback will come; host routine now */
+		g_st.tx_host++;
 		e->crc = pech_cpu_crc32c(seed, data, len);
 		e->state = ST_DONE;
 	}
@@ -266,8 +331,8 @@ int crc32c_msgr_tx_known(struct crc32c_msgr_conn *c, void *msg, uint32_t crc)
 
 	if (!c)
 		return -EINVAL;
-	if (tx_find(c, msg, NULL))
-		return 0;
+	if (tx_find(c, msg))
+		return 1;
 	e = tx_new(c, msg);
 	if (!e)
 		return -ENOMEM;
@@ -277,13 +342,18 @@ int crc32c_msgr_tx_known(struct crc32c_msgr_conn *c, void *msg, uint32_t crc)
 	return 0;
 }
 
+int crc32c_msgr_tx_has(const struct crc32c_msgr_conn *c, const void *msg)
+{
+	return c && tx_find((struct crc32c_msgr_conn *)c, msg) ? 1 : 0;
+}
+
 int crc32c_msgr_tx_footer(struct crc32c_msgr_conn *c, void *msg, uint32_t *crc)
 {
-	struct tx_ent **link = NULL, *e;
+	struct tx_ent *e;
 
 	if (!c || !crc)
 		return -EINVAL;
-	e = tx_find(c, msg, &link);
+	e = tx_find(c, msg);
 	if (!e)
 		return -ENOENT;
 	if (e->state != ST_DONE) {
@@ -293,28 +363,74 @@ int crc32c_msgr_tx_footer(struct crc32c_msgr_conn *c, void *msg, uint32_t *crc)
 		return 0;
 	}
 	*crc = e->crc;
-	*link = e->next;
+	tx_unlink(c, e);
 	free(e);
 	return 1;
 }
 
-void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c)
+/* drop e: released now, or (its CRC still in flight) when the CRC lands */
+static void tx_drop(struct crc32c_msgr_conn *c, struct tx_ent *e)
 {
-	struct tx_ent *e, *n;
+	tx_unlink(c, e);
+	if (e->state == ST_WAIT) {
+		e->conn = NULL; /* the GPU still reads its bytes: released in tx_done */
+		return;
+	}
+	c->release(e->msg);
+	g_st.tx_released++;
+	free(e);
+}
+
+unsigned int crc32c_msgr_tx_cancel(struct crc32c_msgr_conn *c, void *msg)
+{
+	struct tx_ent *e;
+	unsigned int n = 0;
+
+	if (!c)
+		return 0;
+	if (msg) {
+		e = tx_find(c, msg);
+		if (e) {
+			tx_drop(c, e);
+			n = 1;
+		}
+		return n;
+	}
+	while (c->tx) {
+		tx_drop(c, c->tx);
+		++n;
+	}
+	return n;
+}
+
+void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c)
+{
+	struct rx_ent *e, *n;
 
 	if (!c)
 		return;
-	crc32c_msgr_conn_reset(c);
-	for (e = c->tx; e; e = n) {
+	for (e = c->head; e; e = n) {
 		n = e->next;
 		if (e->state == ST_WAIT) {
-			e->conn = NULL; /* the GPU still reads its bytes: released in tx_done */
+			e->conn = NULL; /* the GPU still reads its bytes: released in rx_done */
+			e->next = NULL;
 		} else {
-			c->release(e->msg);
-			g_st.tx_released++;
+			if (e->msg) /* NULL: an in-order skip marker */
+				c->release(e->msg);
+			g_st.rx_released++;
 			free(e);
 		}
 	}
+	c->head = c->tail = NULL;
+	c->npending = 0;
+}
+
+void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c)
+{
+	if (!c)
+		return;
+	crc32c_msgr_conn_reset(c);
+	crc32c_msgr_tx_cancel(c, NULL);
 	free(c);
 }
 

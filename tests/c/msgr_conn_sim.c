@@ -280,7 +280,7 @@ static int try_write(struct sconn *c)
 		c->outq_n--;
 		/* prepare_write_message: header CRC on the host (drop-in), data CRC submitted */
 		f->hdr_crc = crc32c(0, m->hdr, HDR_LEN);
-		if (do_datacrc && crc32c_msgr_tx_submit(c->ad, m, m->data, m->len, 0))
+		if (do_datacrc && crc32c_msgr_tx_submit(c->ad, m, m->data, m->len, 0) < 0)
 			FAIL("%s tx_submit\n", c->name);
 		/* the data on the wire: the receiver's buffer (alloc_msg) */
 		f->src = m;
@@ -689,7 +689,7 @@ int main(int argc, char **argv)
 	 * fault / as a duplicate -- none was dispatched (checked at dispatch) */
 	if (do_datacrc && (nr_detected + nr_dropped_corrupt != nr_corrupted || (nr_corrupted && !nr_detected)))
 		FAIL("corrupted %u, detected %u, dropped %u\n", nr_corrupted, nr_detected, nr_dropped_corrupt);
-	if (!do_datacrc && (st.rx_submitted || st.tx_submitted || st.rx_verified))
+	if (!do_datacrc && (st.rx_submitted || st.tx_submitted || st.rx_verified || st.rx_host || st.tx_host))
 		FAIL("NO_DATA_CRC: the adapter computed CRCs\n");
 	if (do_datacrc && st.rx_unchecked)
 		FAIL("data CRC on: %llu messages went unchecked\n", (unsigned long long)st.rx_unchecked);
@@ -707,14 +707,15 @@ int main(int argc, char **argv)
 	printf("msgr_conn_sim %s: writes %u+%u dispatched, repops %u+%u of %u (%u by concat), corrupted %u detected %u dropped %u, "
 	       "faults %u, "
 	       "dups %u; adapter rx submitted %llu verified %llu bad %llu unchecked %llu released %llu, tx submitted "
-	       "%llu known %llu held %llu; drop-in host calls %llu; %u errors\n",
+	       "%llu known %llu held %llu; host-routed rx %llu tx %llu; drop-in host calls %llu; %u errors\n",
 	       do_datacrc ? "crc" : "nocrc", dispatched_writes[0], dispatched_writes[1], dispatched_repops[0],
 	       dispatched_repops[1], repops_expected, repops_concat, nr_corrupted, nr_detected, nr_dropped_corrupt,
 	       pin[0]->faults + pin[1]->faults + rin[0]->faults + rin[1]->faults,
 	       pin[0]->dups + pin[1]->dups + rin[0]->dups + rin[1]->dups, (unsigned long long)st.rx_submitted,
 	       (unsigned long long)st.rx_verified, (unsigned long long)st.rx_bad, (unsigned long long)st.rx_unchecked,
 	       (unsigned long long)st.rx_released, (unsigned long long)st.tx_submitted,
-	       (unsigned long long)st.tx_known, (unsigned long long)st.tx_held, (unsigned long long)ds.cpu_calls,
+	       (unsigned long long)st.tx_known, (unsigned long long)st.tx_held, (unsigned long long)st.rx_host,
+	       (unsigned long long)st.tx_host, (unsigned long long)ds.cpu_calls,
 	       nr_errors);
 	return nr_errors ? 1 : 0;
 }

@@ -3,6 +3,7 @@
 concatenation.  CPU tests: the algebra and the C test program's build; GPU
 tests: every callback bit-exact against the oracle (the reference loop)."""
 import os
+import re
 import select
 import subprocess
 
@@ -155,8 +156,9 @@ def test_msgr_conn_sim_builds_as_pech_c():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,corrupt", [("crc", "7"), ("crc", "0"), ("nocrc", "0")])
-def test_msgr_connection_state_machine(mode, corrupt):
+@pytest.mark.parametrize("mode,corrupt,host_max", [("crc", "7", None), ("crc", "7", "0"), ("crc", "0", None),
+                                                   ("nocrc", "0", None)])
+def test_msgr_connection_state_machine(mode, corrupt, host_max):
     # tests/c/msgr_conn_sim.c: send-side held footers (a6), receive verify
     # queue with in-order dispatch and acks only after verification (a5, f1),
     # corruption -> -EBADMSG -> fault -> resend (no corrupted dispatch),
@@ -164,9 +166,23 @@ def test_msgr_connection_state_machine(mode, corrupt):
     # NO_DATA_CRC / header-CRC gates (a10); every footer vs the reference chain
     exe = os.path.join(REPO, "build", "msgr_conn_sim")
     assert os.path.exists(exe), "build/msgr_conn_sim is built by `make`"
-    r = subprocess.run([exe, mode, "150", corrupt], capture_output=True, timeout=240)
+    # host_max: the adapter's size routing (crc32c_msgr_set_host_max): by
+    # default payloads <= 16 KiB are checksummed on the host and the larger
+    # ones on the GPU; "0" sends every checked payload to the GPU
+    env = dict(os.environ)
+    if host_max is not None:
+        env["PECH_CRC32C_MSGR_HOST_MAX"] = host_max
+    r = subprocess.run([exe, mode, "150", corrupt], capture_output=True, timeout=240, env=env)
     out = r.stdout.decode() + r.stderr.decode()
     assert r.returncode == 0, out[-4000:]
     assert " 0 errors" in out
     if mode == "crc" and corrupt != "0":
         assert "corrupted 0 " not in out  # the run did inject and catch corruption
+    if mode == "crc":
+        m = re.search(r"rx submitted (\d+) .* tx submitted (\d+) .*host-routed rx (\d+) tx (\d+)", out)
+        rx_gpu, tx_gpu, rx_host, tx_host = map(int, m.groups())
+        assert rx_gpu > 0 and tx_gpu > 0  # sizes above the cutoff went to the GPU
+        if host_max == "0":
+            assert rx_host == 0 and tx_host == 0
+        else:  # 0/1/100/4096/4097-byte payloads stayed on the host
+            assert rx_host > 0 and tx_host > 0

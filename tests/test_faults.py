@@ -1,27 +1,40 @@
-"""Failure paths a healthy GPU never takes, driven by the library's fault
-hook (crc32c_test_inject, api_internal.h pech_fault_site):
+"""Failure paths a healthy GPU never takes, driven by the fault-injection
+hook (crc32c_test_inject, api_internal.h pech_fault_site).  The hook exists
+only in the test build, build/lib_test.so (`make`, -DPECH_TEST_HOOKS): the
+release library cannot be armed.  So every scenario runs in ONE child
+process (this file run as a script, PECH_CRC32C_LIB=build/lib_test.so) and
+each test below checks its scenario's outcome:
 
 * the drop-in crc32c() stays total: a failed GPU leg is recomputed on the
   host, exactly (SURVEY.md §8(b) "Errors": the reference cannot fail,
   include/crc32c.h:88-96);
-* the async layer (ADVICE r1): a failed launch or payload DMA fails the
+* the async layer (ADVICE r1, r2): a failed launch or payload DMA fails the
   payloads of that slot through their callbacks (err < 0), makes the
   context's error sticky, wakes the eventfd, and never strands a later
-  callback; a submission that returns an error gets no callback.
+  callback; a submission that returns an error gets no callback -- also the
+  one whose own submit filled the slot and whose launch failed (under the
+  messenger adapter too: no callback reaches a freed verify-queue entry);
+* a batch whose stream fails after its launch never signals the eventfd;
+  complete() finds it by asking the stream and fails its payloads.
 Run on the GPU box (-m gpu)."""
 import ctypes
+import json
+import os
 import select
+import subprocess
+import sys
+import traceback
 
 import numpy as np
 import pytest
 
-import oracle_lib as O
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TEST_LIB = os.path.join(REPO, "build", "lib_test.so")
+SITE_DROPIN_GPU, SITE_ASYNC_LAUNCH, SITE_ASYNC_DMA, SITE_ASYNC_STREAM = 0, 1, 2, 3
+SLOT_DESCS, SLOT_BYTES = 8192, 32 << 20  # crc32c_async.cpp kSlotDescs / kSlotBytes
 
-pytestmark = pytest.mark.gpu
 
-SITE_DROPIN_GPU, SITE_ASYNC_LAUNCH, SITE_ASYNC_DMA = 0, 1, 2
-
-
+# ---- scenarios (run in the child, on build/lib_test.so) ---------------------
 def inject(site, countdown):
     from pech_amd import _lib
 
@@ -30,14 +43,13 @@ def inject(site, countdown):
     assert L.crc32c_test_inject(site, countdown) == 0
 
 
-@pytest.fixture(autouse=True)
 def disarm():
-    yield
-    for s in (SITE_DROPIN_GPU, SITE_ASYNC_LAUNCH, SITE_ASYNC_DMA):
+    for s in (SITE_DROPIN_GPU, SITE_ASYNC_LAUNCH, SITE_ASYNC_DMA, SITE_ASYNC_STREAM):
         inject(s, 0)
 
 
-def test_dropin_gpu_failure_recomputed_on_host():
+def sc_dropin_gpu_failure_recomputed_on_host():
+    import oracle_lib as O
     import pech_amd as P
 
     rng = np.random.default_rng(41)
@@ -64,7 +76,8 @@ def _wait(ac, timeout=60.0):
         ac.complete()
 
 
-def test_async_launch_failure_fails_its_slot_then_sticky():
+def sc_async_launch_failure_fails_its_slot_then_sticky():
+    import oracle_lib as O
     import pech_amd as P
 
     rng = np.random.default_rng(42)
@@ -80,21 +93,28 @@ def test_async_launch_failure_fails_its_slot_then_sticky():
     for i in (2, 3):
         ac.submit(bufs[i].ctypes.data, bufs[i].size, i, cb(i), keep=bufs[i])
     inject(SITE_ASYNC_LAUNCH, 1)
-    with pytest.raises(P.Crc32cError):
+    try:
         ac.flush()
+        raise AssertionError("flush after an injected launch failure returned 0")
+    except P.Crc32cError:
+        pass
     # the context's error is sticky: later submissions are refused (no callback)
-    with pytest.raises(P.Crc32cError):
+    try:
         ac.submit(bufs[4].ctypes.data, bufs[4].size, 4, cb(4), keep=bufs[4])
+        raise AssertionError("submit on a failed context returned 0")
+    except P.Crc32cError:
+        pass
     _wait(ac)  # the eventfd woke the loop; every accepted payload completed
     assert got[0] == (O.crc(0, bufs[0]), 0)
     assert got[1] == (O.crc(1, bufs[1]), 0)
     assert got[2][1] < 0 and got[3][1] < 0
-    assert 4 not in got
+    assert 4 not in got and ac.stray == 0
     assert list(got) == [0, 1, 2, 3]  # submission order
     ac.close()
 
 
-def test_async_dma_failure_mid_slot():
+def sc_async_dma_failure_mid_slot():
+    import oracle_lib as O
     import pech_amd as P
 
     rng = np.random.default_rng(43)
@@ -108,21 +128,121 @@ def test_async_dma_failure_mid_slot():
     ac.flush()  # payload 0 in flight in its own slot
     ac.submit(pages[1].ptr, pages[1].nbytes, 1, cb(1))  # slot 2, DMA'd
     inject(SITE_ASYNC_DMA, 1)
-    with pytest.raises(P.Crc32cError):  # payload 2's DMA fails: no callback for it
+    try:  # payload 2's DMA fails: no callback for it
         ac.submit(pages[2].ptr, pages[2].nbytes, 2, cb(2))
-    with pytest.raises(P.Crc32cError):  # drain reports the sticky error after the callbacks ran
+        raise AssertionError("submit with a failed DMA returned 0")
+    except P.Crc32cError:
+        pass
+    try:  # drain reports the sticky error after the callbacks ran
         ac.drain()
+        raise AssertionError("drain after a failed slot returned 0")
+    except P.Crc32cError:
+        pass
     assert got[0] == (O.crc(0, pages[0].view), 0)
     assert got[1][1] < 0  # shared the failed slot
-    assert 2 not in got
+    assert 2 not in got and ac.stray == 0
     assert ac.pending() == 0
     ac.close()
     for pg in pages:
         pg.free()
 
 
-def test_async_context_after_failure_is_replaceable():
+def sc_submit_that_fills_the_slot_fails_without_callback():
+    # the payload whose own submit filled the slot
+    # (kSlotDescs pieces) and whose launch failed gets an error return and
+    # NO callback; the slot's earlier payloads get err < 0 callbacks
+    import pech_amd as P
+
+    rng = np.random.default_rng(45)
+    data = rng.integers(0, 256, 64, dtype=np.uint8)
+    ac = P.AsyncCrc()
+    got = {}
+    cb = lambda i: (lambda crc, err: got.__setitem__(i, (crc, err)))  # noqa: E731
+    for i in range(SLOT_DESCS - 1):
+        ac.submit(data.ctypes.data, 64, i, cb(i), keep=data)
+    inject(SITE_ASYNC_LAUNCH, 1)
+    try:
+        ac.submit(data.ctypes.data, 64, SLOT_DESCS - 1, cb(SLOT_DESCS - 1), keep=data)
+        raise AssertionError("the submit that filled the failed slot returned 0")
+    except P.Crc32cError:
+        pass
+    _wait(ac)
+    assert SLOT_DESCS - 1 not in got and ac.stray == 0
+    assert len(got) == SLOT_DESCS - 1 and all(e < 0 for _, e in got.values())
+    ac.close()
+
+
+def sc_msgr_submit_that_fills_the_slot_is_recomputed_once():
+    # the same failure under the messenger adapter (crc32c_msgr.c): the
+    # refused payload is recomputed on the host at once, and since no
+    # callback follows, rx_next may free its entry before complete() runs
+    import oracle_lib as O
+    import pech_amd as P
+    from pech_amd import _lib
+
+    L = _lib.lib()
+    prev = L.crc32c_msgr_set_host_max(0)  # every checked payload to the GPU
+    released = []
+    REL = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    rel = REL(lambda m: released.append(m))
+    ac = P.AsyncCrc()
+    conn = L.crc32c_msgr_conn_create(ac.handle, 16, None, None, ctypes.cast(rel, ctypes.c_void_p))
+    assert conn
+    try:
+        rng = np.random.default_rng(46)
+        big = rng.integers(0, 256, SLOT_BYTES, dtype=np.uint8)  # fills a staging slot by itself
+        want = O.crc(0, big)
+        inject(SITE_ASYNC_LAUNCH, 1)
+        assert L.crc32c_msgr_rx_queue(conn, ctypes.c_void_p(7), big.ctypes.data, big.size, 1, want) == 0
+        msg, crc = ctypes.c_void_p(), ctypes.c_uint32()
+        assert L.crc32c_msgr_rx_next(conn, ctypes.byref(msg), ctypes.byref(crc)) == 1  # recomputed, entry freed
+        assert msg.value == 7 and crc.value == want
+        for _ in range(3):  # no callback may reach the freed entry
+            L.crc32c_async_complete(ac.handle)
+        assert ac.pending() == 0
+        st = _lib.CMsgrStats()
+        L.crc32c_msgr_get_stats(ctypes.byref(st))
+        assert st.rx_host >= 1 and st.rx_verified >= 1 and st.rx_bad == 0
+        assert released == []
+    finally:
+        L.crc32c_msgr_conn_destroy(conn)
+        L.crc32c_msgr_set_host_max(prev)
+        ac.close()
+
+
+def sc_failed_stream_found_by_complete():
+    # a batch whose stream fails after the launch never runs
+    # its host function, so the eventfd stays quiet; complete() (called from
+    # the loop's timer) asks the stream and fails the batch's payloads
+    import oracle_lib as O
+    import pech_amd as P
+
+    rng = np.random.default_rng(47)
+    d = rng.integers(0, 256, 10000, dtype=np.uint8)
+    ac = P.AsyncCrc()
+    got = []
+    ac.submit(d.ctypes.data, d.size, 3, lambda crc, err: got.append((crc, err)), keep=d)
+    ac.flush()
+    ac.drain()
+    assert got == [(O.crc(3, d), 0)]
+    inject(SITE_ASYNC_STREAM, 1)
+    ac.submit(d.ctypes.data, d.size, 4, lambda crc, err: got.append((crc, err)), keep=d)
+    ac.flush()
+    r, _, _ = select.select([ac.fd()], [], [], 1.0)
+    assert not r, "the eventfd fired for a batch whose host function never ran"
+    for _ in range(200):  # the timer
+        ac.complete()
+        if len(got) == 2:
+            break
+        select.select([], [], [], 0.01)
+    assert len(got) == 2 and got[1][1] < 0
+    assert ac.pending() == 0
+    ac.close()
+
+
+def sc_context_after_failure_is_replaceable():
     # a fresh context works after one failed (the failure is per context)
+    import oracle_lib as O
     import pech_amd as P
 
     d = np.random.default_rng(44).integers(0, 256, 70000, dtype=np.uint8)
@@ -132,3 +252,52 @@ def test_async_context_after_failure_is_replaceable():
     ac.drain()
     assert got == [(O.crc(9, d), 0)]
     ac.close()
+
+
+SCENARIOS = [n for n in list(globals()) if n.startswith("sc_")]
+
+
+def child_main():
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for name in SCENARIOS:
+        try:
+            globals()[name]()
+            res[name] = "ok"
+        except Exception:  # noqa: BLE001 -- reported to the parent test
+            res[name] = traceback.format_exc()
+        finally:
+            disarm()
+    print("FAULT_RESULTS " + json.dumps(res), flush=True)
+
+
+# ---- the tests (parent process) ---------------------------------------------
+@pytest.fixture(scope="module")
+def results():
+    assert os.path.exists(TEST_LIB), "build/lib_test.so is built by `make` (__graft_entry__.build())"
+    env = dict(os.environ, PECH_CRC32C_LIB=TEST_LIB)
+    r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__)], capture_output=True, text=True,
+                       timeout=300, env=env)
+    line = [l for l in r.stdout.splitlines() if l.startswith("FAULT_RESULTS ")]
+    assert r.returncode == 0 and line, (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+    return json.loads(line[-1][len("FAULT_RESULTS "):])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SCENARIOS)
+def test_fault_scenario(results, name):
+    assert results[name] == "ok", results[name]
+
+
+def test_release_library_has_no_fault_hook():
+    # failure injection is not exported by the release library
+    out = subprocess.check_output(["nm", "-D", "--defined-only", os.path.join(REPO, "pech_amd", "libpech_crc32c.so")],
+                                  text=True)
+    assert "crc32c_test_inject" not in out
+    if os.path.exists(TEST_LIB):
+        assert "crc32c_test_inject" in subprocess.check_output(["nm", "-D", "--defined-only", TEST_LIB], text=True)
+
+
+if __name__ == "__main__":
+    child_main()
