@@ -34,6 +34,7 @@ import argparse
 import ctypes
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -274,11 +275,17 @@ def main():
                 traffic = prof.get("hbm_bytes_per_launch")
                 break
 
+    # distinct devices over all ranks (a gloo rehearsal puts several ranks on one GPU)
+    ndev = len(set(devids))
+    if dist is not None:
+        alldev = [None] * world
+        dist.all_gather_object(alldev, [(socket.gethostname(), d) for d in devids])
+        ndev = len({x for r in alldev for x in r})
     line = {
         "metric": "CRC32C GiB/s on device-resident object buffers (4 KiB–4 MiB), 1/2/4/8 GPUs",
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world * len(set(devids)),
+        "n_gpus": ndev,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -323,8 +330,23 @@ def main():
         line["sustained"] = {"seconds": round(sec, 2), "steps": steps_done, "streams": nstreams,
                              "value": round(batch_bytes * steps_done * world * len(shards) / sec / (1 << 30), 2),
                              "unit": "GiB/s"}
-    if len(shards) > 1:
+    if len(shards) > 1 and dist is None:
         line["shards_checked"] = shard_parity(shards, offs, sizes, rotate, P)
+    if dist is not None:
+        # every rank checks its own shard against the oracle (outside the
+        # timed region); rank 0 reports how many shards passed
+        try:
+            ok = shard_parity(shards, offs, sizes, rotate, P)
+            bad = 0
+        except SystemExit as e:
+            print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
+            ok, bad = 0, 1
+        t = torch.tensor([ok, bad], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        if int(t[1]):
+            raise SystemExit(f"PARITY FAILURE: {int(t[1])} rank(s) computed CRCs that differ from the reference")
+        line["shards_checked"] = int(t[0])
+        line["ranks"] = world
     if rank == 0 and world == 1 and len(shards) == 1 and launches:
         probe = stream_probe("copy" if dsts else "read", max(1, batch_bytes >> 20))
         if probe:
@@ -553,9 +575,9 @@ def stream_probe(kind, mib):
 
 
 def shard_parity(shards, offs, sizes, rotate, P):
-    """Single-thread multi-shard runs: every shard's last outputs for its
-    first and last buffers against the oracle (test infrastructure, outside
-    the timed region)."""
+    """Multi-shard runs (single-thread, or one rank of a torchrun job): every
+    shard's last outputs for its first and last buffers against the oracle
+    (test infrastructure, outside the timed region)."""
     import torch
 
     sys.path.insert(0, os.path.join(REPO, "tests"))

@@ -200,8 +200,8 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t *t1, uint32_t crc, 
 }
 
 // fused-copy variant: bytes [lo, hi) of the block whose first byte is at
-// `dst` in the destination (heads, tails and buffers without a full aligned
-// piece; the main kernel stores the rest)
+// `dst` in the destination (a partial first piece, the tail, or a buffer
+// without a core; the main kernel stores only whole pieces)
 __device__ __forceinline__ void copy_block(u32x4 v, uint32_t lo, uint32_t hi, uint64_t dst)
 {
 	__attribute__((address_space(1))) uint8_t *d = (__attribute__((address_space(1))) uint8_t *)dst;
@@ -213,9 +213,13 @@ __device__ __forceinline__ void copy_block(u32x4 v, uint32_t lo, uint32_t hi, ui
 	}
 }
 
-// COPY: also dst[b] <- bytes of buffer b (fused CRC + copy); the plan kernel
-// records dl = dst - src per buffer for the main kernel and copies the
-// bytes the main kernel does not (head, tail, or the whole tiny buffer).
+// Per buffer: its row-space descriptor (layout.h) and the part of its CRC
+// outside the core -- the tail R(0, t) (one block load, only for an
+// unaligned end), the seed term x^(8 len) seed (0 for the messenger's zero
+// seeds), or the whole CRC of a buffer without a core.  No GF(2) shift of
+// data: a head is masked in the main kernel.  COPY: also dst[b] <- the
+// bytes of a partial first piece (a second block load) and of the tail,
+// and dl = dst - src for the main kernel.
 template <bool COPY>
 __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, uint32_t n, pech_core *__restrict__ cores,
 					  uint32_t *__restrict__ lrs, uint32_t *__restrict__ partials,
@@ -231,30 +235,25 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	__shared__ uint32_t rmax; // largest core of the chunk (uniformity flag)
 	const uint32_t tid = threadIdx.x;
 	const uint32_t b = blockIdx.x * PECH_CHUNK + tid;
-	// All three loads unconditional (clamped indices) so they are in flight
-	// together: loads under exec-masked branches each got a vmcnt(0) at the
-	// branch's join -- three serial round trips before the first barrier.
+	// loads unconditional (clamped indices) so they are in flight together:
+	// loads under exec-masked branches each got a vmcnt(0) at the join
 	pech_desc d = descs[min(b, n - 1u)];
 	const uint32_t tv1 = consts[PECH_C_TAB1 + (tid & 255u)];
 	const uint32_t tvp = consts[PECH_C_POWB + min(tid, 383u)];
 	if (b >= n)
 		d.len = 0;
-	// The bytes outside the main kernel's rows (head, tail, or a whole buffer
-	// without a full aligned piece) lie in the aligned 16-byte blocks holding
-	// the buffer's first and last bytes: two vector loads in flight together
-	// (a byte loop here cost one global round trip per byte).  An aligned
-	// 16-byte block never crosses a page, so it is readable whenever one of
-	// its bytes is.  A block with nothing to read (an aligned start or end,
-	// an empty buffer whose address may be anything) loads the buffer's own
-	// descriptor instead: aligned batches read no payload here (reading both
-	// blocks of every 4 KiB buffer cost C2 5 % per step).
+	// The tail lies in the aligned 16-byte block at ce (an aligned block never
+	// crosses a page, so it is readable whenever one of its bytes is).  A
+	// buffer with nothing to read there (an aligned end, an empty buffer
+	// whose address may be anything) loads its own descriptor instead.
 	const uint64_t safe = (uint64_t)(descs + min(b, n - 1u));
-	const uint64_t a0 = d.addr & ~(uint64_t)15;
-	const bool needA = d.len != 0 && (d.addr & 15u) != 0;          // head, or a tiny buffer's first block
-	const bool needT = d.len != 0 && ((d.addr + d.len) & 15u) != 0; // tail, or a tiny buffer's last block
-	const uint64_t aT0 = (d.addr + d.len - 1u) & ~(uint64_t)15;
-	const u32x4 vA = *(g_u32x4 *)(needA ? a0 : safe);
-	const u32x4 vT = *(g_u32x4 *)(needT ? aT0 : safe);
+	const uint64_t end = d.addr + d.len, ce = end & ~(uint64_t)15, a0 = d.addr & ~(uint64_t)15;
+	const bool needT = d.len != 0 && (end & 15u) != 0;
+	const u32x4 vT = *(g_u32x4 *)(needT ? ce : safe);
+	u32x4 vA = (u32x4)(0u);
+	const bool hp = COPY && d.len != 0 && (d.addr & 15u) != 0 && a0 != ce; // partial first piece of a core
+	if (COPY)
+		vA = *(g_u32x4 *)(hp ? a0 : safe);
 	if (tid < 256)
 		t1[tid] = tv1;
 	if (tid < 384)
@@ -267,55 +266,33 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	uint32_t rows = 0, cls = 0;
 	pech_core core = {0, 0, 0};
 	if (b < n) {
-		const uint64_t end = d.addr + d.len;
 		rows = pech_core_rows(d.addr, d.len);
-		uint32_t res;
+		const uint32_t t = (uint32_t)(end - ce);
 		int64_t dl = 0;
 		if (COPY) {
 			dl = (int64_t)(dsts[b] - d.addr);
 			deltas[b] = dl;
 		}
+		uint32_t res;
 		if (rows == 0) {
-			// no full aligned piece: the whole buffer here (<= 30 bytes, in
-			// block A and, if it crosses into the next block, block T)
-			// (two blocks only with an unaligned start and end: needA, needT)
-			res = d.seed;
-			if (d.len) {
-				const u32x4 v0 = needA ? vA : vT; // the block holding the first byte
-				const uint32_t o = (uint32_t)(d.addr - a0), e = (uint32_t)min((uint64_t)16u, o + (uint64_t)d.len);
-				res = crc_block(t1, res, v0, o, e);
-				if (aT0 != a0)
-					res = crc_block(t1, res, vT, 0, (uint32_t)(end - aT0));
-				if (COPY) {
-					copy_block(v0, o, e, a0 + dl);
-					if (aT0 != a0)
-						copy_block(vT, 0, (uint32_t)(end - aT0), aT0 + dl);
-				}
-			}
+			// no core: the buffer lies inside the block at ce (<= 15 bytes)
+			res = d.len ? crc_block(t1, d.seed, vT, (uint32_t)(d.addr - ce), t) : d.seed;
+			if (COPY && d.len)
+				copy_block(vT, (uint32_t)(d.addr - ce), t, ce + dl);
 		} else {
-			const uint64_t cs = (d.addr + 15) & ~(uint64_t)15;
-			const uint64_t ce = end & ~(uint64_t)15;
-			const uint32_t h = (uint32_t)(cs - d.addr), t = (uint32_t)(end - ce);
-			// head: the last h bytes of block A (= cs - 16); tail: the first t of block T (= ce)
-			if (COPY) {
-				copy_block(vA, 16u - h, 16u, a0 + dl);
-				copy_block(vT, 0u, t, aT0 + dl);
-			}
-			res = 0;
-			if (d.seed)
-				res ^= shift_bytes(powb, d.len, d.seed);
-			if (h)
-				res ^= shift_bytes(powb, (uint64_t)d.len - h, crc_block(t1, 0, vA, 16u - h, 16u));
+			// seed term R(s, D) = x^(8|D|) s ^ R(0, D), and the tail R(0, t)
+			res = d.seed ? shift_bytes(powb, d.len, d.seed) : 0u;
 			if (t)
 				res ^= crc_block(t1, 0, vT, 0u, t);
-			// rows on the line grid (layout.h): vp leading virtual pieces in
-			// row 0, zt trailing ones in the last row
-			const uint64_t vb = cs & ~(uint64_t)(PECH_ROW_BYTES - 1u);
-			const uint32_t vp = (uint32_t)((cs - vb) >> 4);
-			const uint32_t zt = rows * 8u - (uint32_t)((ce - vb) >> 4);
-			core.vbase = vb;
+			if (COPY) {
+				if (hp)
+					copy_block(vA, (uint32_t)(d.addr - a0), 16u, a0 + dl);
+				if (t)
+					copy_block(vT, 0u, t, ce + dl);
+			}
+			core.addr = d.addr;
 			core.rows = rows;
-			core.meta = PECH_META(b, vp, t, zt);
+			core.meta = PECH_META(b, pech_core_zt(d.addr, d.len, rows), t);
 			cls = pech_size_class(rows);
 		}
 		out[b] = res;
@@ -379,7 +356,9 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 		// locates any row by division and pools its work (PECH_ITEM_ROWS)
 		const uint32_t cnt = min(PECH_CHUNK, n - blockIdx.x * PECH_CHUNK);
 		const bool uni = nz == cnt && (uint64_t)nz * rmax == (uint64_t)total && total != 0;
-		nzs[blockIdx.x] = nz | (uni ? PECH_NZ_UNIFORM : 0u);
+		// the small cores (< PECH_SPLIT_ROWS rows: classes 0-7) come first
+		const uint32_t nsmall = wcnt[8u * PECH_WAVES_PER_WG];
+		nzs[blockIdx.x] = nz | (nsmall << PECH_NS_SHIFT) | (uni ? PECH_NZ_UNIFORM : 0u);
 	}
 }
 
@@ -488,20 +467,21 @@ extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
 // Per lane: `ad` = address of this lane's piece in the run's first row, `nl`
 // rows to load (>= 1), `nu` rows to use (0 = idle group: its loads repeat
 // another group's rows and its state is ignored), `zoff` != 0 = the first
-// row's piece is a virtual zero (it may lie before the buffer, so row 0 is
-// loaded from ad + zoff -- the first real piece -- and zeroed), `m` = bytes
+// row's piece lies wholly before the buffer (row 0 is loaded from ad + zoff
+// -- the first real piece -- and zeroed), `zh` = its first zh bytes lie
+// before the buffer (zeroed), `zl` = the lane's piece of the run's last row
+// lies past the core's end (a trailing virtual piece, zeroed), `m` = bytes
 // from the run's end to the buffer's end (final shift; negative when the
-// run ends in the buffer's last row and its zt trailing virtual pieces
-// outnumber the tail bytes), `orig` = output slot, `zl` = the lane's piece
-// of the run's last row is a trailing virtual piece (read as zero, never
-// stored).
+// run ends in the core's last row and its zt trailing virtual pieces
+// outnumber the tail bytes), `orig` = output slot.  Zeroed bytes are never
+// stored by the fused copy.
 // Uniform: T / nmin = max / min of nu over the active groups (T == 0: no
 // step), and the wave's cursor after the step.
 struct Step {
 	uint64_t ad;
-	uint32_t mp;  // rows after the run << 4 | tail bytes   (m = 128 rows + tail - 16 zt)
+	uint32_t mp;  // rows after the run << 7 | zt << 4 | tail   (m = 128 rows + tail - 16 zt)
 	uint32_t nl, nu;
-	uint32_t oz;  // orig | (zoff / 16) << 20 | zl << 23 | zt << 24   (zoff <= 112, zt < 8)
+	uint32_t oz;  // orig | (zoff / 16) << 20 | zh << 23 | zl << 27   (zoff <= 112, zh < 16)
 	uint32_t T, nmin;
 	uint32_t pos, lr, rem;
 	uint64_t dad; // fused copy: destination of this lane's piece in row 0 (ad + dst - src)
@@ -542,14 +522,46 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 
 static_assert(PECH_MAIN_WAVES % 4 == 0 && PECH_MAIN_WAVES <= 16, "waves per workgroup: 4, 8, 12 or 16");
 
+// Step.oz bits of lane g8 when its run starts at the buffer's row 0 (first):
+// lb leading bytes of the row lie before the buffer -- pieces below lb/16
+// wholly (zoff redirect), lb%16 bytes of piece lb/16 (zh)
+__device__ __forceinline__ uint32_t head_bits(bool first, uint32_t g8, uint32_t lb)
+{
+	const uint32_t vp = lb >> 4;
+	if (!first)
+		return 0u;
+	return g8 < vp ? (vp - g8) << 20 : (g8 == vp ? (lb & 15u) << 23 : 0u);
+}
+
+// ... and when it ends the core (last): the last zt pieces of the row lie
+// past it (trailing virtual pieces, zeroed)
+__device__ __forceinline__ uint32_t tail_bits(bool last, uint32_t g8, uint32_t zt)
+{
+	return last && g8 >= 8u - zt ? 1u << 27 : 0u;
+}
+
+// v with its bytes [0, kb) kept and [kb, 16) zeroed (0 <= kb <= 16)
+__device__ __forceinline__ u32x4 keep_below(u32x4 v, uint32_t kb)
+{
+	u32x4 r;
+#pragma unroll
+	for (uint32_t j = 0; j < 4; ++j) {
+		const uint32_t k = min(kb - min(kb, 4u * j), 4u);
+		r[j] = v[j] & (k >= 4u ? 0xFFFFFFFFu : (1u << (8u * k)) - 1u);
+	}
+	return r;
+}
+
 // Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
 // the destination offset of each group's buffer (deltas[orig], scalar loads).
 // PRE: `spec` holds cores[ppos + grp] (loaded at kernel entry); a step that
 // starts at ppos takes its descriptors from it instead of loading them.
+// grid: static shares, whose small-buffer steps lie on a grid of 8 positions.
 template <bool COPY, bool PRE = false>
 __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
 					  const uint32_t *lds, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
-					  uint32_t g8, uint32_t grp, const pech_core &spec = pech_core{}, uint32_t ppos = 0)
+					  uint32_t g8, uint32_t grp, bool grid, const pech_core &spec = pech_core{},
+					  uint32_t ppos = 0)
 {
 	Step S;
 	int64_t dl = 0;
@@ -579,15 +591,21 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 		else
 			cd = cores[pos];
 #ifdef PECH_DEBUG_BOUNDS
-		if (hit && (cd.rows != cores[pos + grp].rows || cd.vbase != cores[pos + grp].vbase))
+		if (hit && (cd.rows != cores[pos + grp].rows || cd.addr != cores[pos + grp].addr))
 			printf("PECH OOB preloaded descriptor pos %u grp %u\n", pos, grp);
 #endif
 		const uint32_t rows0 = uni(cd.rows);
-		const uint64_t vb0 = uni64(cd.vbase);
+		const uint64_t a0 = uni64(cd.addr);
+		const uint64_t vb0 = a0 & ~(uint64_t)(PECH_ROW_BYTES - 1u);
+		const uint32_t lb0 = (uint32_t)a0 & (PECH_ROW_BYTES - 1u);
 		const uint32_t meta0 = uni(cd.meta);
-		const uint32_t vp0 = PECH_META_VP(meta0);
+		const uint32_t zt0 = PECH_META_ZT(meta0);
 		const uint32_t avail0 = rows0 - lr;
-		if (avail0 >= PECH_SPLIT_ROWS && rem >= 64u) {
+		// A large buffer (or what is left of it) goes to 8 slices when at least
+		// 64 of its rows are to be walked: a remainder below PECH_SPLIT_ROWS
+		// walked by group 0 alone left 7 groups idle (up to 255 rows; 19 % of
+		// the row slots of a C4-like mix in tests/kernel_model.py).
+		if (rows0 >= PECH_SPLIT_ROWS && min(avail0, rem) >= 64u) {
 			// one large buffer (portion): 8 contiguous slices, one per group
 			const uint32_t P = min(avail0, rem);
 			const uint32_t q = P >> 3, rm = P & 7u;
@@ -596,17 +614,15 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			S.ad = vb0 + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
 			S.nl = nn;
 			S.nu = nn;
-			const uint32_t zt0 = PECH_META_ZT(meta0);
-			const bool zl0 = st + nn == rows0 && g8 >= 8u - zt0; // this slice ends the buffer
-			S.oz = PECH_META_ORIG(meta0) | ((st == 0 && g8 < vp0) ? (vp0 - g8) << 20 : 0u) |
-			       (zl0 ? 1u << 23 : 0u) | (zt0 << 24);
-			S.mp = ((rows0 - st - nn) << 4) | PECH_META_TAIL(meta0);
+			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) |
+			       tail_bits(st + nn == rows0, g8, zt0); // the first / this slice ends the buffer
+			S.mp = ((rows0 - st - nn) << 7) | (meta0 >> 16 & 0x70u) | PECH_META_TAIL(meta0);
 			S.T = q + (rm ? 1u : 0u);
 			S.nmin = q;
 			if (COPY)
 				dl = deltas[PECH_META_ORIG(meta0)];
 #ifdef PECH_DEBUG_BOUNDS
-			S.blo = vb0 + 16u * vp0;
+			S.blo = vb0 + 16u * (lb0 >> 4);
 			S.bhi = vb0 + (uint64_t)rows0 * PECH_ROW_BYTES;
 #endif
 			rem -= P;
@@ -625,8 +641,8 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
 			int64_t mdl = 0;
 			if (hit) {
-				vlo = (uint32_t)spec.vbase;
-				vhi = (uint32_t)(spec.vbase >> 32);
+				vlo = (uint32_t)spec.addr;
+				vhi = (uint32_t)(spec.addr >> 32);
 				mrows = spec.rows;
 				mmeta = spec.meta;
 				if (COPY) {
@@ -639,8 +655,8 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 				for (uint32_t j = 0; j < 8; ++j) {
 					const pech_core dj = cores[pos + j];
 					const bool mine = grp == j;
-					vlo = mine ? uni((uint32_t)dj.vbase) : vlo;
-					vhi = mine ? uni((uint32_t)(dj.vbase >> 32)) : vhi;
+					vlo = mine ? uni((uint32_t)dj.addr) : vlo;
+					vhi = mine ? uni((uint32_t)(dj.addr >> 32)) : vhi;
 					mrows = mine ? uni(dj.rows) : mrows;
 					mmeta = mine ? uni(dj.meta) : mmeta;
 					if (COPY) {
@@ -653,7 +669,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 				}
 			}
 			pech_core my;
-			my.vbase = ((uint64_t)vhi << 32) | vlo;
+			my.addr = ((uint64_t)vhi << 32) | vlo;
 			my.rows = mrows;
 			my.meta = mmeta;
 			const uint32_t myp = pos + grp;
@@ -669,7 +685,12 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			// group, from its lane 0), by DPP: no LDS round trips
 			const uint32_t incl = wave_incl_scan(g8 == 0 ? avail : 0u);
 			const uint32_t pre = incl - avail;
-			const uint32_t nu = pre >= rem ? 0u : min(avail, rem - pre);
+			// grid (static shares): a step of small buffers is walked whole
+			// by the wave whose share holds its middle row (the first row of
+			// its position kcut/2; prologue in main_body), else not at all
+			const bool whole = grid && rows0 < PECH_SPLIT_ROWS;
+			const bool own = lane_value(pre, 8u * (kcut >> 1)) < rem;
+			const uint32_t nu = whole ? (own ? avail : 0u) : (pre >= rem ? 0u : min(avail, rem - pre));
 			// the step's longest and shortest run: 8 lane reads (group-uniform values)
 			uint32_t tmax = 0, tmin = 0xFFFFFFFFu;
 #pragma unroll
@@ -680,28 +701,29 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			}
 			S.T = tmax;
 			S.nmin = tmin;
-			const uint32_t used = min(lane_value(incl, 63), rem);
-			const uint32_t myvp = PECH_META_VP(my.meta);
-			uint32_t zp;
+			// (whole: the share's rest at most; a step not owned ends the range)
+			const uint32_t used = whole && !own ? rem : min(lane_value(incl, 63), rem);
+			const uint32_t mylb = (uint32_t)my.addr & (PECH_ROW_BYTES - 1u);
+			const uint64_t myvb = my.addr & ~(uint64_t)(PECH_ROW_BYTES - 1u);
+			const uint32_t myzt = PECH_META_ZT(my.meta);
 			if (nu) {
-				S.ad = my.vbase + (uint64_t)mylr * PECH_ROW_BYTES + 16u * g8;
+				S.ad = myvb + (uint64_t)mylr * PECH_ROW_BYTES + 16u * g8;
 				S.nl = nu;
-				zp = (mylr == 0 && g8 < myvp) ? myvp - g8 : 0u;
+				S.oz = PECH_META_ORIG(my.meta) | head_bits(mylr == 0, g8, mylb) |
+				       tail_bits(mylr + nu == myrows, g8, myzt); // the run ends the buffer
 			} else {
-				// idle groups reload group 0's rows (valid memory), state ignored
+				// idle groups reload group 0's rows (valid memory: the redirect
+				// of row 0's pieces before the buffer kept), state ignored
 				S.ad = vb0 + (uint64_t)lr * PECH_ROW_BYTES + 16u * g8;
 				S.nl = min(avail0, rem);
-				zp = (lr == 0 && g8 < vp0) ? vp0 - g8 : 0u;
+				S.oz = head_bits(lr == 0, g8, lb0) & (7u << 20);
 			}
 			S.nu = nu;
 			dl = mdl;
-			const uint32_t myzt = PECH_META_ZT(my.meta);
-			const bool zl = nu != 0 && mylr + nu == myrows && g8 >= 8u - myzt; // the run ends the buffer
-			S.oz = PECH_META_ORIG(my.meta) | (zp << 20) | (zl ? 1u << 23 : 0u) | (myzt << 24);
-			S.mp = ((myrows - mylr - nu) << 4) | PECH_META_TAIL(my.meta);
+			S.mp = ((myrows - mylr - nu) << 7) | (my.meta >> 16 & 0x70u) | PECH_META_TAIL(my.meta);
 #ifdef PECH_DEBUG_BOUNDS
-			const uint64_t bv = nu ? my.vbase : vb0;
-			S.blo = bv + 16u * (nu ? myvp : vp0);
+			const uint64_t bv = nu ? myvb : vb0;
+			S.blo = bv + 16u * ((nu ? mylb : lb0) >> 4);
 			S.bhi = bv + (uint64_t)(nu ? myrows : rows0) * PECH_ROW_BYTES;
 #endif
 			rem -= used;
@@ -721,8 +743,10 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 
 #define STEP_ZOFF(S) (((S).oz >> 16) & 0x70u) // (zoff/16) << 20 -> zoff
 #define STEP_ORIG(S) ((S).oz & 0xFFFFFu)
-#define STEP_ZL(S) (((S).oz >> 23) & 1u)
-#define STEP_M(S) ((int64_t)((uint64_t)((S).mp >> 4) * PECH_ROW_BYTES + ((S).mp & 15u)) - 16 * (int64_t)((S).oz >> 24))
+#define STEP_ZH(S) (((S).oz >> 23) & 15u)
+#define STEP_HEAD(S) (((S).oz >> 20) & 0x7Fu) // row 0's piece is not wholly the buffer's (zoff or zh)
+#define STEP_ZL(S) ((S).oz >> 27)
+#define STEP_M(S) ((int64_t)((uint64_t)((S).mp >> 7) * PECH_ROW_BYTES + ((S).mp & 15u)) - (int64_t)((S).mp & 0x70u))
 
 // Ring discipline: row k of a step lives in ring slot k % PECH_U and the
 // lookahead is PECH_U-1 rows.  The iteration that consumes row k first issues
@@ -806,7 +830,7 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 	}
 }
 
-// A trailing virtual piece (past the core's end, in the buffer's last row)
+// A trailing virtual piece (past the core's end, in the core's last row)
 // counts as zero; only the ragged and last blocks of a step can hold a run's
 // last row.
 __device__ __forceinline__ u32x4 zl_mask(const Step &S, uint32_t row, u32x4 v)
@@ -819,8 +843,10 @@ __device__ __forceinline__ bool zl_keep(const Step &S, uint32_t row)
 }
 
 // Fused copy: the consumed piece of row `row` of the lane's run goes to its
-// destination (S.dad: source + dst - src).  Virtual pieces (row 0 with zoff) and rows past
-// nu (clamped prefetch, idle groups) are never stored.
+// destination (S.dad: source + dst - src).  Pieces not wholly the buffer's
+// (row 0 with zoff or zh -- the plan kernel copies the bytes of a partial
+// one --, trailing virtual pieces) and rows past nu (clamped prefetch, idle
+// groups) are never stored.
 template <bool COPY>
 __device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, bool ok)
 {
@@ -902,7 +928,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	pech_core spec; // cores[pg + grp] (pg + 7 may run into lrs: workspace memory, used only if in the chunk)
 	{
 		const u32x4 v = ((const u32x4 *)cores)[pg + grp];
-		spec.vbase = ((uint64_t)v.y << 32) | v.x;
+		spec.addr = ((uint64_t)v.y << 32) | v.x;
 		spec.rows = v.z;
 		spec.meta = v.w;
 	}
@@ -926,7 +952,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		const bool real = lane * 16u + k < nchunks;
 		const uint32_t nzf = real ? nv4[k >> 2][k & 3u] : PECH_NZ_UNIFORM;
 		pc[k] = real ? pv4[k >> 2][k & 3u] : 0u;
-		nc[k] = nzf & ~PECH_NZ_UNIFORM;
+		nc[k] = nzf & ~PECH_NZ_UNIFORM; // non-empty | small cores << PECH_NS_SHIFT
 		uflag = uflag && (nzf & PECH_NZ_UNIFORM) != 0u;
 		lsum += pc[k];
 	}
@@ -935,25 +961,32 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// Uniform batch (every chunk flagged by the plan kernel, all with chunk
 	// 0's rows per buffer): position p holds rows [p U0, (p+1) U0), so any row
 	// is located by a division, and the workgroup pools its rows in items.
-	const uint32_t nz0 = lane_value(nc[0], 0); // (lane values: wave-uniform, as the pool needs)
+	const uint32_t nz0 = lane_value(nc[0], 0) & PECH_NZ_MASK; // (lane values: wave-uniform, as the pool needs)
 	const uint32_t U0 = nz0 ? lane_value(pc[0], 0) / nz0 : 0u;
 	bool uok = uflag;
 #pragma unroll
 	for (uint32_t k = 0; k < 16; ++k)
-		uok = uok && (uint64_t)nc[k] * U0 == (uint64_t)pc[k];
+		uok = uok && (uint64_t)(nc[k] & PECH_NZ_MASK) * U0 == (uint64_t)pc[k];
 	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
 	STAMP(t_scan);
 	// Every wave gets an equal share of the batch's rows (at least rpw_min).
-	const uint32_t rpw_eq = Rtot ? (Rtot - 1u) / W + 1u : 0u;
-	const uint32_t rpw = max(rpw_min, rpw_eq);
-	const uint64_t wg0 = (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+	// Large batches: workgroup b gets rows [b Rtot / G, (b+1) Rtot / G) --
+	// proportional, not b * ceil(Rtot / W): the rounding drifted by up to a
+	// row per wave, a whole step of 8 small buffers after a few hundred
+	// waves, so some waves walked an extra step (2 -> 3 on unaligned
+	// 4,100-byte buffers) and set the launch's end.  Small batches: shares
+	// of rpw_min rows, the last workgroups idle.
+	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_min;
+	const uint32_t rpw = prop ? 0u : rpw_min;
+	const uint64_t wg0 = prop ? (uint64_t)blockIdx.x * Rtot / gridDim.x : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
 	if (wg0 >= Rtot)
 		return; // whole workgroup idle (small batch)
 	u32x4 ring[U];
 	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
 	// equal contiguous pieces (age-weighted shares measured no better,
 	// profiles/r01/ab_v5.txt).
-	const uint32_t wg_rows = (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+	const uint32_t wg_rows = prop ? (uint32_t)((uint64_t)(blockIdx.x + 1u) * Rtot / gridDim.x - wg0)
+				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
 	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
 	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
 	// Uniform batches: a wave starts on its share's head [r0, t) and then
@@ -972,17 +1005,19 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 							     PECH_ITEM_ROWS
 					       : 0u;
 #endif
-	const uint32_t rem_all = jmax ? share_head(r0, r1) - r0 : r1 - r0;
+	uint32_t rem_all = jmax ? share_head(r0, r1) - r0 : r1 - r0;
 
 	// nz table for plan_step: every wave writes all of it (the same values)
 	// and reads back only its own writes until the barrier below
 #pragma unroll
 	for (uint32_t k = 0; k < 4; ++k)
 		*(u32x4 *)(lds + L_NZ / 4u + lane * 16u + 4u * k) =
-			u32x4{nc[4 * k], nc[4 * k + 1], nc[4 * k + 2], nc[4 * k + 3]}; // braces: a parenthesised list is a comma splat
+			u32x4{nc[4 * k], nc[4 * k + 1], nc[4 * k + 2], nc[4 * k + 3]} & PECH_NZ_MASK; // braces: a parenthesised list is a comma splat
 
 	uint32_t p0 = 0, lr0 = 0;
 	bool found = false;
+	// the start chunk's prefix, non-empty and small cores, and rows (grid snap below)
+	uint32_t jj = 0, pjj = 0, nzjj = 0, nsjj = 0;
 	if (rem_all) {
 		// The speculated position first, checked exactly: buffer pg holds
 		// row r0 iff its global offset (chunk prefix + lrs[pg]) <= r0 <
@@ -997,10 +1032,15 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		}
 		const uint32_t og = lane_value(prec, lc) + uni(lrg);
 		const uint32_t rg = uni(spec.rows); // lane 0: cores[pg]
-		if (cg < nchunks && (pg & 1023u) < lane_value(nzc, lc) && og <= r0 && r0 - og < rg) {
+		if (cg < nchunks && (pg & 1023u) < (lane_value(nzc, lc) & PECH_NZ_MASK) && og <= r0 && r0 - og < rg) {
 			p0 = pg;
 			lr0 = r0 - og;
 			found = true;
+			jj = cg;
+			pjj = lane_value(prec, lc);
+			nzjj = lane_value(nzc, lc);
+			nsjj = nzjj >> PECH_NS_SHIFT;
+			nzjj &= PECH_NZ_MASK;
 		}
 	}
 	if (rem_all && !found) {
@@ -1020,6 +1060,11 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		const uint32_t j = Lj * 16u + lane_value(cnt, Lj) - 1u;
 		pj = lane_value(pj, Lj);
 		nzj = lane_value(nzj, Lj);
+		nsjj = nzj >> PECH_NS_SHIFT;
+		nzj &= PECH_NZ_MASK;
+		jj = j;
+		pjj = pj;
+		nzjj = nzj;
 		const uint32_t rr = r0 - pj;
 		if (j != cg && lane * 16u < nzj) { // speculation missed: the start chunk's row offsets now
 #pragma unroll
@@ -1048,8 +1093,35 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			       blockIdx.x, wave, r0, j, cg, nchunks, nzj, cpos, rr, cores[min(p0, nchunks * PECH_CHUNK - 1u)].rows);
 #endif
 	}
+	// Static shares (no pool): the small cores of a chunk (its first nsjj
+	// positions) are walked in whole steps of 8 positions on a grid from the
+	// chunk start, each by the wave whose share holds the step's middle row
+	// (the first row of its position cnt/2).  A wave starting inside a small
+	// step walks it from its start if it owns it, else starts at the next
+	// grid point.  Shares cut inside small buffers left a partial first and
+	// last step per wave, with idle groups (unaligned 4,100-byte buffers: 2
+	// steps per wave became 3, +37 % per launch), and ownership by the first
+	// row flipped with +-1 row of jitter when shares and steps nearly align.
+	const bool grid = jmax == 0u;
+	if (grid && rem_all) {
+		const uint32_t local = p0 & 1023u;
+		if (local < nsjj) {
+			const uint32_t k0 = local & ~7u, cnt = min(8u, nsjj - k0), k1 = min(nsjj, k0 + 8u);
+			// the step's middle row, its first row and the next grid point's,
+			// by scalar loads issued together (wave-uniform addresses)
+			const uint32_t *cl = lrs + jj * PECH_CHUNK;
+			const uint32_t omid = uni(cl[k0 + cnt / 2u]), o0 = uni(cl[k0]);
+			const uint32_t o1 = uni(k1 < nzjj ? cl[k1] : partials[jj]);
+			const bool own = pjj + omid >= r0;
+			const uint32_t roff = pjj + (own ? o0 : o1); // (before r0 if this wave owns the step)
+			rem_all = r1 > roff ? r1 - roff : 0u;
+			const uint32_t l2 = own ? k0 : k1;
+			p0 = l2 < nzjj ? jj * PECH_CHUNK + l2 : (jj + 1u) * PECH_CHUNK;
+			lr0 = 0;
+		}
+	}
 	STAMP(t_find);
-	Step S = plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, spec, pg);
+	Step S = plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
 	STAMP(t_plan);
 	if (S.T)
 		RING_PRIME(S, ring);
@@ -1096,8 +1168,15 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #endif
 	while (S.T) {
 		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-		if (STEP_ZOFF(S))
-			ring[0] = (u32x4)(0u);
+		// row 0's bytes before the buffer are zeros (free: leading zeros):
+		// zoff -> the whole piece, zh -> its first zh bytes; on 64-bit halves
+		{
+			const uint32_t sh = STEP_ZOFF(S) ? 128u : 8u * STEP_ZH(S);
+			uint64_t lo = ((uint64_t)ring[0].y << 32) | ring[0].x, hi = ((uint64_t)ring[0].w << 32) | ring[0].z;
+			lo &= sh >= 64u ? 0ull : ~0ull << sh;
+			hi &= sh >= 128u ? 0ull : (sh <= 64u ? ~0ull : ~0ull << (sh - 64u));
+			ring[0] = u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+		}
 		const uint32_t nblk = (S.T + U - 1) / U;
 		const uint32_t last = S.nl - 1u;
 		uint32_t blk = 0;
@@ -1122,7 +1201,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 					horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
 #pragma unroll
 				for (uint32_t i = 0; i < U; ++i)
-					st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_ZOFF(S)));
+					st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_HEAD(S)));
 #pragma unroll
 				for (uint32_t i = 0; i + 1 < U; ++i)
 					ring[i] = LD_PIECE(S, base + (U + i) * PECH_ROW_BYTES, 2);
@@ -1132,7 +1211,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
 				horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
-				st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_ZOFF(S)));
+				st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_HEAD(S)));
 			}
 		}
 		// ragged blocks: clamped prefetch, predicated update
@@ -1146,7 +1225,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 				for (uint32_t i = 0; i < U; ++i)
 					st_piece<COPY>(S, r + i, ring[i],
-						       r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)) && zl_keep(S, r + i));
+						       r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i));
 #pragma unroll
 				for (uint32_t i = 0; i + 1 < U; ++i)
 					ring[i] = LD_PIECE(S, row_addr(S.ad, min(r + U + i, last), STEP_ZOFF(S)), 3);
@@ -1158,7 +1237,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 					LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
 				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 				st_piece<COPY>(S, r + i, ring[i],
-					       r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)) && zl_keep(S, r + i));
+					       r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i));
 			}
 		}
 		// last block: its first load is this step's last row, the rest
@@ -1186,7 +1265,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				}
 			}
 		}
-		const Step N = plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp);
+		const Step N = plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
 		if constexpr (COPY) { // block discipline: this block's rows and stores, then the next step's loads
 			const bool more = N.T != 0;
 			const Step &L = more ? N : S;
@@ -1196,13 +1275,13 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i)
-				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && (r + i != 0 || !STEP_ZOFF(S)) && zl_keep(S, r + i));
+				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i));
 #pragma unroll
 			for (uint32_t i = 1; i < U; ++i)
 				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
 		} else {
 			horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
-			st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_ZOFF(S)) && zl_keep(S, r));
+			st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_HEAD(S)) && zl_keep(S, r));
 			// Branch-free on purpose: with no next step the prefetch re-reads
 			// this step's last row (valid memory, never used).  An if/else here
 			// let LLVM sink the shared Horner code into a join block, which
@@ -1347,6 +1426,6 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.15 gfx950 rows128 wave-steps(8x8-lane groups) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.16 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS);
 }

@@ -1,28 +1,30 @@
 /*
  * layout.h -- geometry shared by the host library and the gfx950 kernels.
  *
- * Split of one buffer D = (addr, len, seed) (gf2.h identities):
- *   head h = [addr, cs)        cs = align16(addr)              (< 16 bytes)
- *   core c = [cs, ce)          ce = align16_down(addr + len)   (16-byte pieces)
- *   tail t = [ce, addr + len)                                  (< 16 bytes)
- *   crc32c(seed, D) = x^(8|t|) * R(0, c)                      <- main kernel
- *                   ^ x^(8 len) * seed
- *                   ^ x^(8(|c|+|t|)) * R(0, h) ^ R(0, t)      <- plan kernel
- * Buffers with no full aligned piece (len < 16 or spanning < one aligned
- * 16-byte block) are checksummed entirely by the plan kernel (<= 30 bytes).
- *
- * Row space.  The core's 16-byte pieces are grouped in 128-byte ROWS (8
- * pieces), on the 128-byte line grid, so every row load is one whole HBM
- * line: row 0 is the line holding cs (vbase = align128_down(cs)), its first
- * vp pieces (vp < 8) are virtual leading zeros, which do not change R(0, .);
- * the last row's last zt pieces (zt < 8) lie past ce, still inside that
- * line, and are read as zeros -- trailing zeros multiply R by x^(128 zt),
- * which the run's final shift undoes (x^(8 |t| - 128 zt), inverse powers
- * when negative).  (Until v0.12 rows were right-aligned to ce, so a core
- * whose end was not line-aligned put every row across two lines: +15 %
- * HBM traffic and +13 % time on such batches.)  One 8-lane GROUP of a wave
- * walks rows of one buffer; lane g8 of the group holds piece g8 of every
- * row as four 4-byte register "streams".
+ * Split of one buffer D = (addr, len, seed) (v0.16):
+ *   core c = [addr, ce)    ce = align16_down(addr + len)   <- main kernel
+ *   tail t = [ce, addr + len)                (< 16 bytes)  <- plan kernel
+ *   crc32c(seed, D) = x^(8|t|) * R(0, c) ^ R(0, t) ^ x^(8 len) * seed
+ * The core is viewed on the 128-byte line grid: ROWS are the lines holding
+ * it, row 0 at vbase = align128_down(addr), so every row load is one whole
+ * HBM line.  One 8-lane GROUP of a wave walks rows of one buffer; lane g8 of
+ * the group holds 16-byte piece g8 of every row as four 4-byte register
+ * "streams".  The rows' bytes outside the core are read as zeros:
+ *   lb = addr - vbase leading bytes of row 0 -- pieces below lb/16 wholly,
+ *        the first lb%16 bytes of piece lb/16: leading zeros do not change
+ *        R(0, .) (gf2.h), so a head costs nothing;
+ *   zt whole trailing pieces of the last row past ce: trailing zeros
+ *        multiply R by x^(128 zt), which the last run's final shift undoes
+ *        (x^(8|t| - 128 zt), inverse powers when negative).
+ * A buffer with no core (it lies inside one aligned 16-byte block) is
+ * checksummed entirely by the plan kernel.  The plan kernel reads one block
+ * per buffer with an unaligned end (its tail) and no other payload byte.
+ * (Until v0.15 it also checksummed the < 16-byte head from a second block,
+ * with a GF(2) shift of up to six 32-step multiplies: 13.6 us of plan and 5 %
+ * more HBM traffic on unaligned 4,100-byte buffers.  Until v0.12 rows were
+ * right-aligned to the core end instead of the line grid: +15 % traffic.)
+ * The fused copy stores only whole pieces in the main kernel; its plan
+ * kernel copies the bytes of a partial first piece and of the tail.
  */
 #ifndef PECH_CRC32C_LAYOUT_H
 #define PECH_CRC32C_LAYOUT_H
@@ -48,6 +50,8 @@
 #define PECH_POOL_ROWS 512u       /* uniform batches: at most this many of a wave's rows are pooled */
 #endif
 #define PECH_NZ_UNIFORM 0x80000000u /* nzs[] flag: every buffer of the chunk has a core of the same rows */
+#define PECH_NZ_MASK 0x7FFu         /* nzs[] bits 0-10: non-empty cores of the chunk */
+#define PECH_NS_SHIFT 11u           /* nzs[] bits 11-21: of them, cores below PECH_SPLIT_ROWS (sorted first) */
 #define PECH_SMALL_MAX 65536u     /* drop-in crc32c(): one-launch path up to this */
 #define PECH_DROPIN_CPU_MAX_DEFAULT (4u << 20) /* drop-in crc32c(): host routine up to this */
 /* payload of one launch: rows (128 B) are counted in 32 bits, so < 512 GiB */
@@ -73,17 +77,15 @@ struct pech_desc {
 
 /* per-buffer core descriptor written by the plan kernel, in row-space order */
 struct pech_core {
-	uint64_t vbase; /* address of row 0, piece 0 (may precede the core)      */
-	uint32_t rows;  /* rows of the core (0: buffer fully done by the plan)   */
-	uint32_t meta;  /* orig (bits 0-19) | vp (20-22) | tail (24-27) | zt (28-30) */
+	uint64_t addr;  /* first byte of the buffer (and core); row 0 at addr & ~127 */
+	uint32_t rows;  /* lines holding the core (0: none, done by the plan)     */
+	uint32_t meta;  /* orig (bits 0-19) | zt (20-22) | tail (23-26)          */
 };
 
-#define PECH_META(orig, vp, t, zt) \
-	((orig) | ((uint32_t)(vp) << 20) | ((uint32_t)(t) << 24) | ((uint32_t)(zt) << 28))
+#define PECH_META(orig, zt, t) ((orig) | ((uint32_t)(zt) << 20) | ((uint32_t)(t) << 23))
 #define PECH_META_ORIG(m) ((m) & 0xFFFFFu)
-#define PECH_META_VP(m) (((m) >> 20) & 7u)
-#define PECH_META_TAIL(m) (((m) >> 24) & 15u)
-#define PECH_META_ZT(m) (((m) >> 28) & 7u)
+#define PECH_META_ZT(m) (((m) >> 20) & 7u)
+#define PECH_META_TAIL(m) (((m) >> 23) & 15u)
 
 #ifdef __HIPCC__
 #define LAYOUT_FN __host__ __device__ inline
@@ -91,15 +93,19 @@ struct pech_core {
 #define LAYOUT_FN static inline
 #endif
 
-/* rows (128-byte lines) holding the core of buffer (addr, len); 0 if it has
- * no full aligned piece */
+/* rows (128-byte lines) holding the core [addr, align16_down(addr + len))
+ * of buffer (addr, len); 0 if it has none */
 LAYOUT_FN uint32_t pech_core_rows(uint64_t addr, uint32_t len)
 {
-	const uint64_t cs = (addr + 15) & ~(uint64_t)15;
 	const uint64_t ce = (addr + len) & ~(uint64_t)15;
-	if (ce <= cs)
-		return 0;
-	return (uint32_t)((ce - (cs & ~(uint64_t)127) + 127) >> 7);
+	return ce > addr ? (uint32_t)(((addr & 127u) + (ce - addr) + 127u) >> 7) : 0u;
+}
+
+/* whole 16-byte pieces of the core's last row past its end (0..7) */
+LAYOUT_FN uint32_t pech_core_zt(uint64_t addr, uint32_t len, uint32_t rows)
+{
+	const uint64_t ce = (addr + len) & ~(uint64_t)15;
+	return (uint32_t)(((uint64_t)rows * 128u - (addr & 127u) - (ce - addr)) >> 4);
 }
 
 /* size class used to order buffers inside a plan chunk (similar row counts
@@ -120,7 +126,7 @@ LAYOUT_FN uint32_t pech_size_class(uint32_t rows)
  *   cores    pech_core[slots]        sorted core descriptors per chunk
  *   lrs      u32[slots]              chunk-local exclusive row scan
  *   partials u32[PECH_MAX_CHUNKS]    rows per chunk
- *   nzs      u32[PECH_MAX_CHUNKS]    non-empty cores per chunk | PECH_NZ_UNIFORM
+ *   nzs      u32[PECH_MAX_CHUNKS]    non-empty cores per chunk | small ones << 11 | PECH_NZ_UNIFORM
  *   deltas   i64[slots]              fused copy: destination - source per buffer
  * slots = nch * PECH_CHUNK, nch = ceil(m / PECH_CHUNK). */
 struct pech_ws {

@@ -3,8 +3,11 @@ pech_amd/csrc/crc32c_kernels.hip (plan + main kernels), statement by
 statement, used by tests/test_kernel_model.py to check -- on the CPU, before a
 kernel ever runs on a GPU -- that
 
-  * every 16-byte load the main kernel issues lies inside the real core of
-    the buffer it is working on (no read before/after a buffer: a GPU fault),
+  * every 16-byte load the main kernel issues lies inside the lines holding
+    the buffer it is working on, from its first (aligned) piece on (no read
+    before/after a buffer: a GPU fault),
+  * the first row's bytes before the buffer are zeroed (whole pieces, and
+    the head's first addr%16 bytes),
   * every core row of every buffer is consumed by exactly one lane-group,
   * every run's final shift targets the right buffer end.
 
@@ -44,15 +47,17 @@ def share_head(a, b, item=None, pool=None):
     item, pool = item or ITEM, pool or POOL
     return min(b, max(a + item, b - min(pool, b - a)))
 NZ_UNIFORM = 0x80000000
+NZ_MASK = 0x7FF            # nzs[c] bits 0-10: non-empty cores of chunk c
+NS_SHIFT = 11              # bits 11-21: of them, small ones (< PECH_SPLIT_ROWS rows), sorted first
 
 
 def core_rows(addr, ln):
-    """rows (128-byte lines) holding the core (layout.h pech_core_rows)"""
-    cs = (addr + 15) & ~15
+    """rows (128-byte lines) holding the core [addr, align16_down(addr + len))
+    (layout.h pech_core_rows, v0.16: the head is part of the core, masked)"""
     ce = (addr + ln) & ~15
-    if ce <= cs:
+    if ce <= addr:
         return 0
-    return (ce - (cs & ~127) + 127) >> 7
+    return ((addr & 127) + (ce - addr) + 127) >> 7
 
 
 def size_class(rows):
@@ -81,14 +86,14 @@ def plan(descs, rng=None):
             rows = core_rows(addr, ln)
             if rows == 0:
                 continue
-            cs = (addr + 15) & ~15
             ce = (addr + ln) & ~15
-            vbase = cs & ~127  # rows on the line grid
-            vp = (cs - vbase) >> 4
+            vbase = addr & ~127  # rows on the line grid
+            lb = addr - vbase    # leading bytes of row 0 before the buffer
+            vp, zh = lb >> 4, lb & 15
             zt = rows * 8 - ((ce - vbase) >> 4)
             t = addr + ln - ce
-            items.append(dict(vbase=vbase, rows=rows, orig=b, vp=vp, zt=zt, tail=t, cs=cs, ce=ce,
-                              cls=size_class(rows)))
+            items.append(dict(vbase=vbase, rows=rows, orig=b, vp=vp, zh=zh, zt=zt, tail=t, addr=addr, ce=ce,
+                              a0=vbase + 16 * vp, cls=size_class(rows)))
         order = []
         for cls in range(13):
             group = [it for it in items if it["cls"] == cls]
@@ -115,7 +120,9 @@ def plan(descs, rng=None):
         cnt = min(n, (c + 1) * CHUNK) - c * CHUNK
         rmax = max((it["rows"] for it in order), default=0)
         uni = len(order) == cnt and len(order) * rmax == acc and acc != 0
-        nzs.append(len(order) | (NZ_UNIFORM if uni else 0))
+        nsmall = sum(1 for it in order if it["rows"] < SPLIT)
+        assert all(it["rows"] < SPLIT for it in order[:nsmall])  # the small ones come first
+        nzs.append(len(order) | (nsmall << NS_SHIFT) | (NZ_UNIFORM if uni else 0))
     return cores, lrs, partials, nzs
 
 
@@ -174,7 +181,7 @@ def find_start(lrs, pref, nzs, r):
     """find_start_wave: chunk by binary search of the prefix, then the count
     of the chunk's row offsets <= the chunk-local row (one wave-wide read of
     all PECH_CHUNK offsets, entries past nz excluded)."""
-    nzs = [z & ~NZ_UNIFORM for z in nzs]
+    nzs = [z & NZ_MASK for z in nzs]
     nchunks = len(nzs)
     clo, chi = 0, nchunks
     while chi - clo > 1:
@@ -201,14 +208,15 @@ def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None):
     weights = weights or C["PECH_SLOT_W"]
     waves = waves or WAVES_PER_WG
     W = ncu * waves
-    rpw = max(rpw_min, (Rtot + W - 1) // W)
+    prop = Rtot >= W * rpw_min  # kernel: proportional workgroup ranges, else rpw_min shares
+    rpw = rpw_min
     tot = slot_cw(waves, weights)
     out = []
     for b in range(ncu):
-        wg0 = b * waves * rpw
+        wg0 = b * Rtot // ncu if prop else b * waves * rpw
         if wg0 >= Rtot:
             continue
-        wg_rows = min(waves * rpw, Rtot - wg0)
+        wg_rows = (b + 1) * Rtot // ncu - wg0 if prop else min(waves * rpw, Rtot - wg0)
         for w in range(waves):
             out.append((wg0 + wg_rows * slot_cw(w, weights) // tot,
                         wg0 + wg_rows * slot_cw(w + 1, weights) // tot))
@@ -228,7 +236,7 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
     # rows per buffer -> items of ITEM rows: each wave's share's first item by
     # its owner, the rest from the workgroup pool (claim c: item 1 + c//16 of
     # share c%16; which wave takes a claim does not matter for coverage)
-    nz = [z & ~NZ_UNIFORM for z in nzs]
+    nz = [z & NZ_MASK for z in nzs]
     U0 = partials[0] // nz[0] if nz and nz[0] else 0
     uniform = bool(U0) and all((z & NZ_UNIFORM) and n * U0 == p for z, n, p in zip(nzs, nz, partials))
     ranges = wave_ranges(Rtot, ncu, rpw_min, weights)
@@ -239,7 +247,12 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
         for r0, r1 in shares:
             if r1 > r0:
                 pos, lr = find_start(lrs, pref, nzs, r0)
-                walk(cores, nzs, pos, lr, share_head(r0, r1) - r0 if jmax else r1 - r0, U, events)
+                if jmax:
+                    walk(cores, nzs, pos, lr, share_head(r0, r1) - r0, U, events)
+                else:
+                    pos, lr, rem = snap_to_grid(lrs, pref, nzs, pos, lr, r0, r1)
+                    if rem:
+                        walk(cores, nzs, pos, lr, rem, U, events, grid=True)
         if jmax > 1:
             for c in range(WAVES_PER_WG * (jmax - 1)):
                 j, sh = 1 + c // WAVES_PER_WG, c % WAVES_PER_WG
@@ -252,9 +265,31 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
     return events
 
 
-def walk(cores, nzs, pos, lr, rem, U, events):
-    """plan_step + run of one sub-range (pos, lr, rem)."""
-    nzs = [z & ~NZ_UNIFORM for z in nzs]
+def snap_to_grid(lrs, pref, nzs, pos, lr, r0, r1):
+    """Kernel prologue, non-uniform batches: small buffers (< PECH_SPLIT_ROWS
+    rows, the first nsmall positions of a chunk) are walked in whole steps of
+    8 positions on a grid from the chunk start; a step belongs to the wave
+    whose share holds its middle row (the first row of its position
+    cnt/2).  A wave starting inside a small step k walks it if it owns it
+    (from the step's start, before r0), else starts at the next grid point."""
+    c, local = pos >> 10, pos & 1023
+    nz, ns = nzs[c] & NZ_MASK, (nzs[c] >> NS_SHIFT) & NZ_MASK
+
+    def roff(l):
+        return pref[c] + (lrs[c * CHUNK + l] if l < nz else pref[c + 1] - pref[c])
+    if local < ns:
+        k0 = local & ~7
+        cnt = min(8, ns - k0)
+        start = k0 if roff(k0 + cnt // 2) >= r0 else min(ns, k0 + 8)
+        pos = c * CHUNK + start if start < nz else (c + 1) * CHUNK
+        return pos, 0, max(0, r1 - roff(start))
+    return pos, lr, r1 - r0
+
+
+def walk(cores, nzs, pos, lr, rem, U, events, grid=False):
+    """plan_step + run of one sub-range (pos, lr, rem).  grid: a step of
+    small buffers that starts inside the range is walked whole."""
+    nzs = [z & NZ_MASK for z in nzs]
     if True:
         guard = 0
         while rem:
@@ -268,7 +303,10 @@ def walk(cores, nzs, pos, lr, rem, U, events):
             rows0 = cd["rows"]
             avail0 = rows0 - lr
             assert avail0 > 0
-            if avail0 >= SPLIT and rem >= 64:
+            # a large buffer (or what is left of it) goes to 8 slices when at
+            # least 64 of its rows are to be walked: a remainder walked by
+            # group 0 alone left 7 groups idle (up to 255 rows)
+            if rows0 >= SPLIT and min(avail0, rem) >= 64:
                 P = min(avail0, rem)
                 q, rm = P >> 3, P & 7
                 T = q + (1 if rm else 0)
@@ -281,9 +319,10 @@ def walk(cores, nzs, pos, lr, rem, U, events):
                         for row, z in loads:
                             events.append(("load", cd, cd["vbase"] + (st + row) * ROW + 16 * g8 + (zoff if z else 0)))
                         zl = st + nn == rows0 and g8 >= 8 - cd["zt"]
+                        zh = cd["zh"] if (st == 0 and g8 == cd["vp"]) else 0
                         for row in used:
                             events.append(("use", cd["orig"], st + row, g8,
-                                           (zoff != 0 and row == 0) or (zl and row == nn - 1)))
+                                           (zoff != 0 and row == 0) or (zl and row == nn - 1), zh if row == 0 else 0))
                     events.append(("finish", cd["orig"], st + nn,
                                    (rows0 - st - nn) * ROW + cd["tail"] - 16 * cd["zt"]))
                 rem -= P
@@ -305,10 +344,17 @@ def walk(cores, nzs, pos, lr, rem, U, events):
                 kcut = next((g for g in range(8) if cut[g]), 8)
                 avails = [(mys[g][1] - (lr if g == 0 else 0)) if g < kcut else 0 for g in range(8)]
                 pres = [sum(avails[:g]) for g in range(8)]
-                nus = [0 if pres[g] >= rem else min(avails[g], rem - pres[g]) for g in range(8)]
+                whole = grid and rows0 < SPLIT
+                if whole:  # a grid step of small buffers whose middle lies in the range: all of it
+                    assert lr == 0 and (pos & 7) == 0, (pos, lr)
+                    nus = list(avails) if pres[kcut // 2] < rem else [0] * 8
+                else:
+                    nus = [0 if pres[g] >= rem else min(avails[g], rem - pres[g]) for g in range(8)]
+                if whole and not any(nus):
+                    break  # the step is the next wave's: this range is done (kernel: S.T == 0)
                 T = max(nus)
                 nmin = min(x for x in nus if x) if any(nus) else 0xFFFFFFFF
-                used_rows = min(pres[7] + avails[7], rem)
+                used_rows = sum(nus) if whole else min(pres[7] + avails[7], rem)
                 assert used_rows == sum(nus)
                 n0 = min(avail0, rem)
                 for grp in range(8):
@@ -326,13 +372,14 @@ def walk(cores, nzs, pos, lr, rem, U, events):
                         for row, z in loads:
                             events.append(("load", buf, base + row * ROW + (zoff if z else 0)))
                         zl = nu != 0 and mylr + nu == myrows and g8 >= 8 - my["zt"]
+                        zh = my["zh"] if (mylr == 0 and g8 == my["vp"]) else 0
                         for row in used:
                             events.append(("use", my["orig"], mylr + row, g8,
-                                           (zoff != 0 and row == 0) or (zl and row == nu - 1)))
+                                           (zoff != 0 and row == 0) or (zl and row == nu - 1), zh if row == 0 else 0))
                     if nu:
                         events.append(("finish", my["orig"], mylr + nu,
                                        (myrows - mylr - nu) * ROW + my["tail"] - 16 * my["zt"]))
-                rem -= used_rows
+                rem = 0 if whole and not used_rows else rem - min(used_rows, rem)
                 if rem:
                     pos += kcut
                     lr = 0

@@ -39,7 +39,8 @@ def test_torchrun_two_ranks_real_kernels():
     """bench.py's N>1 driver under torchrun with the real kernels: two ranks
     share GPU 0 over gloo (PECH_BENCH_BACKEND=gloo; the driver's N>1 runs use
     RCCL with one GPU per rank).  Rendezvous, barriers, MAX-over-ranks timing
-    and rank 0's single JSON line; each rank checksums its own shard."""
+    and rank 0's single JSON line; each rank checksums its own shard and
+    checks it against the oracle (shards_checked)."""
     env = dict(os.environ, PECH_BENCH_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2", *COMMON],
@@ -48,6 +49,9 @@ def test_torchrun_two_ranks_real_kernels():
     lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
     assert len(lines) == 1, lines  # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    # n_gpus counts distinct devices: both ranks are on GPU 0
+    assert d["n_gpus"] == 1 and d["ranks"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    # each rank checked its own shard against the oracle
+    assert d["shards_checked"] == 2
     assert d["config"]["parallelism"].startswith("shard2")
     assert "cpu_baseline" not in d  # rank 0 at N=1 only

@@ -1,8 +1,8 @@
 """CPU checks of the main kernel's work decomposition through the shadow
 model (tests/kernel_model.py): loads stay inside the lines holding each
-buffer's core (never before its first real piece), every row piece is
-consumed exactly once, the pieces outside the core count as zeros, and
-shifts target the buffer end."""
+buffer's core (never before its first piece), every row piece is consumed
+exactly once, the pieces and head bytes outside the core count as zeros,
+and shifts target the buffer end."""
 import collections
 import random
 
@@ -23,15 +23,18 @@ def check(descs, ncu=4, seed=0, weights=None, U=None):
     for e in ev:
         if e[0] == "load":
             _, buf, a = e
-            # past ce only inside the core's last line (trailing virtual pieces)
-            assert buf["cs"] <= a and a + 16 <= buf["vbase"] + buf["rows"] * KM.ROW, (buf, a)
+            # from the aligned piece holding the buffer's first byte; past ce
+            # only inside the core's last line (trailing virtual pieces)
+            assert buf["a0"] <= a and a + 16 <= buf["vbase"] + buf["rows"] * KM.ROW, (buf, a)
             assert a % KM.ROW // 16 == (a - buf["vbase"]) % KM.ROW // 16  # rows on the line grid
         elif e[0] == "use":
-            _, orig, row, g8, virt = e
+            _, orig, row, g8, virt, zh = e
             c = byorig[orig]
             used[(orig, row, g8)] += 1
             piece = row * 8 + g8
             assert virt == (piece < c["vp"] or piece >= c["rows"] * 8 - c["zt"]), (orig, row, g8)
+            # bytes of the piece before the buffer's first byte, zeroed in place
+            assert zh == (c["addr"] - c["a0"] if piece == c["vp"] else 0), (orig, row, g8, zh)
         elif e[0] == "finish":
             _, orig, endrow, m = e
             c = byorig[orig]

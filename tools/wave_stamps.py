@@ -17,6 +17,8 @@ elif cfg == "c4":  # bench.py's c4_sizes: equal bytes per class, shuffled with s
     sizes = np.asarray(sizes, dtype=np.int64)
 elif cfg == "c2-1g":
     sizes = np.full(262144, 4096, dtype=np.int64)
+elif cfg == "c2-odd":  # bench.py's c2-odd: 4,100-byte buffers back to back (unaligned starts and ends)
+    sizes = np.full(65536, 4100, dtype=np.int64)
 else:
     sizes = np.full(65536, 4096, dtype=np.int64)
 offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
