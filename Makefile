@@ -12,7 +12,7 @@ LIB = pech_amd/libpech_crc32c.so
 HOST_OBJ = build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o build/crc32c_msgr.o
 OBJ = build/crc32c_kernels.o $(HOST_OBJ)
 
-all: $(LIB) oracle build/msgr_sim build/msgr_conn_sim build/dropin_kat build/coro_stack build/dropin_bench \
+all: $(LIB) oracle build/msgr_sim build/msgr_conn_sim build/dropin_kat build/coro_stack build/dropin_bench build/launch_cost \
      build/lib_dbg.so build/lib_test.so build/hbm_probe build/sched_probe
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
@@ -105,6 +105,12 @@ build/dropin_bench: tools/c/dropin_bench.c oracle/crc32c_oracle.c include/pech_c
 	@mkdir -p build
 	gcc -std=gnu89 -O2 -Wall -Werror -fno-strict-aliasing -Iinclude tools/c/dropin_bench.c oracle/crc32c_oracle.c \
 		-Lpech_amd -lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
+
+# bench tool: host CPU per HIP call of an async-layer slot
+build/launch_cost: tools/c/launch_cost.c include/pech_crc32c.h $(LIB)
+	@mkdir -p build
+	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ tools/c/launch_cost.c \
+		-Lpech_amd -lpech_crc32c -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
 
 oracle:
 	$(MAKE) -C oracle all

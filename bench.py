@@ -86,6 +86,10 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams that consecutive batches alternate over (own workspace each) in the timed "
                          "pass that gives `value`; a one-stream pass always gives the per-launch roofline")
+    ap.add_argument("--api", choices=["auto", "planned", "small"], default="auto",
+                    help="device entry point: planned = crc32c_dev_batch_ws_async (plan + main kernel), small = "
+                         "crc32c_dev_batch_small_async (direct kernel, one launch); auto = small when every buffer "
+                         "is below 32 KiB, as the async layer routes its slots")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
     ap.add_argument("--data", choices=["random", "zeros", "ones"], default="random",
@@ -151,6 +155,7 @@ def main():
     batch_bytes = int(sizes.sum())
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     maxs = max(1, args.streams)
+    small_api = args.op == "crc" and (args.api == "small" or (args.api == "auto" and int(sizes.max()) < (32 << 10)))
 
     class Shard:
         """One device's batches: `rotate` distinct resident batches of random
@@ -188,6 +193,8 @@ def main():
                 if self.dsts:
                     P.dev_copy_batch_ws_async(self.descs[i % rotate], self.dsts[i % rotate][1],
                                               self.outs[i % rotate], self.wss[k], stream=self.streams[k])
+                elif small_api:
+                    P.dev_batch_small_async(self.descs[i % rotate], self.outs[i % rotate], stream=self.streams[k])
                 else:
                     P.dev_batch_ws_async(self.descs[i % rotate], self.outs[i % rotate], self.wss[k],
                                          stream=self.streams[k])
@@ -301,10 +308,13 @@ def main():
                                    f"{','.join(map(str, devids))}, no collective" if args.single_thread else
                                    f"shard{world} (independent buffers per GPU, no collective)"),
                    "streams": nstreams,
+                   "api": "crc32c_dev_batch_small_async" if small_api else
+                          ("crc32c_dev_copy_batch_ws_async" if dsts else "crc32c_dev_batch_ws_async"),
                    "kernel": P.version()},
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "pech_crc32c_main_copy" if dsts else "pech_crc32c_main",
+                     "kernel": "pech_crc32c_main_copy" if dsts else
+                               ("pech_crc32c_direct" if small_api else "pech_crc32c_main"),
                      "bytes_per_launch": algo_bytes, "avg_launch_us": round(avg_kernel_s * 1e6, 2),
                      "launch_us_p10_p50_p90": [round(float(np.percentile(samples, q)), 2) for q in (10, 50, 90)]
                      if len(samples) else None,
@@ -494,24 +504,32 @@ def msgr_path(args, buf0, offs, sizes, outs, P):
 
 
 def msgr_c_bench(args, size, count):
-    """The messenger adapter's rate from C (build/msgr_sim bench): `count`
-    payloads of `size` bytes in crc32c_pages memory, one crc32c_async_submit
-    each (flush every 64), eventfd drain; zero-copy and DMA modes.  The C
-    program checks every result of its warm-up pass against the oracle."""
+    """The messenger-side rate and CPU cost from C (build/msgr_sim bench):
+    `count` payloads of `size` bytes in crc32c_pages memory per pass, flushed
+    every 64 and completed from an epoll loop, through the async layer (DMA
+    and zero-copy), the messenger adapter (its size routing at the default),
+    and the drop-in's host routine.  Reported per mode: GiB/s, payloads/s,
+    CPU microseconds per payload of the calling thread (pech's one OS thread)
+    and of the process, submit -> result latency p50/p99.  The C program
+    checks every result against the oracle."""
     import subprocess
 
     exe = os.path.join(REPO, "build", "msgr_sim")
+    count = max(1, min(count, (256 << 20) // max(size, 1)))
     res = {}
-    for mode, zc in (("zerocopy", 1), ("dma", 0)):
-        r = subprocess.run([exe, "bench", str(size), str(count), str(zc), str(args.host_passes)],
+    for mode, m in (("dma", 0), ("zerocopy", 1), ("adapter", 2), ("host", 3)):
+        r = subprocess.run([exe, "bench", str(size), str(count), str(m), str(args.host_passes)],
                            capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             raise SystemExit(f"msgr_sim bench failed ({r.returncode}): {r.stdout} {r.stderr}")
-        res[mode] = json.loads(r.stdout.strip().splitlines()[-1])
-    return {"zerocopy": res["zerocopy"]["GiBps"], "dma": res["dma"]["GiBps"], "unit": "GiB/s",
-            "payloads_per_s": {"zerocopy": res["zerocopy"]["payloads_per_s"], "dma": res["dma"]["payloads_per_s"]},
-            "path": f"C: crc32c_async_submit per {size}-byte payload from crc32c_pages memory, flush every 64, "
-                    "drain via eventfd (build/msgr_sim bench); zerocopy: kernel reads pinned payloads below 1 MiB in place, larger ones DMA'd",
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        res[mode] = {k: d[k] for k in ("GiBps", "payloads_per_s", "thread_cpu_us_per_payload",
+                                       "process_cpu_us_per_payload", "latency_us_p50", "latency_us_p99")}
+    return {"payload_bytes": size, "modes": res, "zerocopy": res["zerocopy"]["GiBps"], "dma": res["dma"]["GiBps"],
+            "unit": "GiB/s",
+            "path": f"C: {size}-byte payloads in crc32c_pages memory, flush every 64, epoll loop on the eventfd "
+                    "(build/msgr_sim bench); dma/zerocopy: crc32c_async_submit per payload; adapter: "
+                    "crc32c_msgr_rx_queue/rx_next (host routine up to its cutoff); host: the drop-in crc32c()",
             "payloads": count, "passes": args.host_passes, "matches_oracle": True}
 
 

@@ -97,8 +97,22 @@ int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32
 int crc32c_dev_batch_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n,
 			   void *stream);
 
+/*
+ * Small-buffer device batch: as crc32c_dev_batch_async, in ONE kernel launch
+ * with no workspace (no plan kernel; the descriptors are read where they
+ * lie), so any number of streams may use it concurrently and it can be
+ * captured in a graph.  Balanced for batches whose buffers are all below
+ * 32 KiB (the messenger's front/middle/data segments and small-object
+ * payloads); correct for any batch, but a larger buffer is walked by one
+ * 8-lane group alone -- route those to crc32c_dev_batch_async.  The results
+ * are stored (d_out needs no initialisation).
+ */
+int crc32c_dev_batch_small_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n,
+				 void *stream);
+
 /* Workspace the device batch needs for n buffers, and the explicit-workspace
- * form (for concurrent streams or graph capture).  d_workspace must be
+ * form (for concurrent streams or graph capture; the internal-workspace forms
+ * are refused inside a capture, -EINVAL).  d_workspace must be
  * 256-byte aligned (hipMalloc memory is) and used by one launch at a time. */
 size_t crc32c_dev_workspace_bytes(unsigned int n);
 int crc32c_dev_batch_ws_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n,

@@ -39,6 +39,8 @@ SIGNATURES = {
                                      ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                      ctypes.c_uint, ctypes.c_uint]),
     "crc32c_dev_batch_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
+    "crc32c_dev_batch_small_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint,
+                                                    ctypes.c_void_p]),
     "crc32c_dev_workspace_bytes": (ctypes.c_size_t, [ctypes.c_uint]),
     "crc32c_dev_batch_ws_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p,
                                                  ctypes.c_size_t, ctypes.c_void_p]),

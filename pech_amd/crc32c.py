@@ -17,7 +17,7 @@ from ._lib import CDesc, Crc32cError, check, lib
 
 __all__ = [
     "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
-    "dev_batch_ws_async", "dev_copy_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
+    "dev_batch_small_async", "dev_batch_ws_async", "dev_copy_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
     "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc", "set_cpu_max", "stats",
 ]
 
@@ -109,6 +109,21 @@ def dev_batch_async(descs, out, stream=None):
         stream = torch.cuda.current_stream(descs.device)
     check(lib().crc32c_dev_batch_async(descs.data_ptr(), out.data_ptr(), n, stream.cuda_stream),
           "crc32c_dev_batch_async")
+
+
+def dev_batch_small_async(descs, out, stream=None):
+    """The small-buffer device batch (crc32c_dev_batch_small_async): one
+    launch, no workspace, graph-capturable; balanced for buffers below
+    32 KiB, correct for any."""
+    import torch
+
+    n = descs.shape[0]
+    if out.numel() < n or out.element_size() != 4:
+        raise ValueError("out must hold n 32-bit words")
+    if stream is None:
+        stream = torch.cuda.current_stream(descs.device)
+    check(lib().crc32c_dev_batch_small_async(descs.data_ptr(), out.data_ptr(), n, stream.cuda_stream),
+          "crc32c_dev_batch_small_async")
 
 
 def workspace_bytes(n):

@@ -14,7 +14,7 @@
 // plan + main kernels for n device descriptors on `stream`, explicit
 // workspace (pech_ws_bytes(n) bytes, 256-byte aligned); current device
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-				     size_t ws_bytes, hipStream_t stream);
+				     size_t ws_bytes, hipStream_t stream, bool small = false);
 // set the thread's crc32c_last_error() text
 PECH_HIDDEN void pech_internal_set_err(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 

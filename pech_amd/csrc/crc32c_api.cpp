@@ -37,6 +37,8 @@ extern "C" hipError_t pech_launch_main(uint32_t, const pech_ws *, const uint32_t
 				       hipStream_t, hipEvent_t, hipEvent_t);
 
 extern "C" const char *pech_kernel_tag(void);
+extern "C" hipError_t pech_launch_direct(const pech_desc *, uint32_t, const uint32_t *, uint32_t *, uint32_t,
+					 hipStream_t, hipEvent_t, hipEvent_t);
 extern "C" hipError_t pech_launch_small(const void *, uint32_t, uint32_t, const uint32_t *, uint32_t *, uint32_t,
 					hipStream_t);
 
@@ -282,23 +284,51 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 
 // A device batch on the internal workspace, on the caller's stream: ordered
 // after the previous user of the workspace when that was another stream
-// (two streams must never share it concurrently).  Inside a graph
-// capture the caller orders the replays (no event edges into the graph).
+// (two streams must never share it concurrently).  Refused inside
+// a graph capture: a replay would use the workspace outside this
+// ordering, and a later reserve could free it under the graph -- captured
+// batches take the _ws_ forms (own workspace) or crc32c_dev_batch_small_async
+// (none).
 static int launch_internal_ws(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n,
 			      hipStream_t stream, const uint64_t *d_dsts)
 {
+	if (capturing(stream)) {
+		set_err("the internal workspace cannot be captured in a graph: use the _ws_ forms "
+			"(own workspace) or crc32c_dev_batch_small_async");
+		return -EINVAL;
+	}
 	int rc = ws_reserve(c, n);
 	if (rc)
 		return rc;
-	const bool cap = capturing(stream);
-	if (!cap && c->ws_used && c->ws_stream != stream)
+	if (c->ws_used && c->ws_stream != stream)
 		HIP_TRY(hipStreamWaitEvent(stream, c->ws_ev, 0));
 	if ((rc = launch_batch(c, d_descs, d_out, n, c->d_ws, c->ws_bytes, stream, d_dsts)))
 		return rc;
-	if (!cap) {
-		HIP_TRY(hipEventRecord(c->ws_ev, stream));
-		c->ws_stream = stream;
-		c->ws_used = true;
+	HIP_TRY(hipEventRecord(c->ws_ev, stream));
+	c->ws_stream = stream;
+	c->ws_used = true;
+	return 0;
+}
+
+// The direct kernel (no plan kernel, no workspace): small-buffer batches,
+// in launches of at most PECH_MAX_BATCH descriptors (output slots are 20 bits)
+static int launch_small(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, hipStream_t stream)
+{
+	for (unsigned int off = 0; off < n; off += PECH_MAX_BATCH) {
+		const unsigned int m = (n - off) < PECH_MAX_BATCH ? (n - off) : PECH_MAX_BATCH;
+		TimedLaunch tl{};
+		if (g_timing) {
+			if (!c->free_events.empty()) {
+				tl = c->free_events.back();
+				c->free_events.pop_back();
+			} else {
+				HIP_TRY(hipEventCreate(&tl.a));
+				HIP_TRY(hipEventCreate(&tl.b));
+			}
+		}
+		HIP_TRY(pech_launch_direct(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, stream, tl.a, tl.b));
+		if (g_timing)
+			c->pending.push_back(tl);
 	}
 	return 0;
 }
@@ -307,14 +337,14 @@ static int launch_internal_ws(DevCtx *c, const pech_desc *d_descs, uint32_t *d_o
 // internal entry points for crc32c_async.cpp (hidden: not part of the C-ABI)
 
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-				     size_t ws_bytes, hipStream_t stream)
+				     size_t ws_bytes, hipStream_t stream, bool small)
 {
 	std::lock_guard<std::mutex> lk(g_mu);
 	DevCtx *c = nullptr;
 	int rc = ctx_get(&c);
 	if (rc)
 		return rc;
-	return launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream);
+	return small ? launch_small(c, d_descs, d_out, n, stream) : launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream);
 }
 
 PECH_HIDDEN void pech_internal_set_err(const char *fmt, ...)
@@ -919,6 +949,24 @@ int crc32c_dev_batch_ws_async(const struct crc32c_desc *d_descs, uint32_t *d_out
 		if (rc)
 			return rc;
 		return launch_batch(c, (const pech_desc *)d_descs, d_out, n, d_ws, ws_bytes, (hipStream_t)stream);
+	});
+}
+
+int crc32c_dev_batch_small_async(const struct crc32c_desc *d_descs, uint32_t *d_out, unsigned int n, void *stream)
+{
+	if (n == 0)
+		return 0;
+	if (!d_descs || !d_out) {
+		set_err("crc32c_dev_batch_small_async: invalid arguments");
+		return -EINVAL;
+	}
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		return launch_small(c, (const pech_desc *)d_descs, d_out, n, (hipStream_t)stream);
 	});
 }
 

@@ -4,11 +4,12 @@
 // Data path of one async context (up to four staging slots in flight, each
 // with its own HIP stream and workspace, so small batches overlap):
 //   submit()   places the payload in the slot being filled -- pageable bytes
-//              are packed into the slot's pinned staging buffer (one CPU
-//              copy), crc32c_pages bytes are DMA'd straight from where they
-//              lie (or, with CRC32C_ASYNC_ZEROCOPY, read by the kernel in
-//              place over the host link) -- and records one descriptor per
-//              piece.  A payload larger than what a slot has left is cut
+//              and crc32c_pages payloads below 32 KiB are packed into the
+//              slot's pinned staging buffer (one CPU copy, one H2D per slot),
+//              larger crc32c_pages payloads are DMA'd straight from where
+//              they lie (or, with CRC32C_ASYNC_ZEROCOPY, read by the kernel
+//              in place over the host link) -- and records one descriptor
+//              per piece.  A payload larger than what a slot has left is cut
 //              into pieces; piece 0 carries the seed, later pieces seed 0.
 //   flush()    H2D of the packed staging runs, plan + main kernels (the plan
 //              reads the descriptors in place from pinned memory), D2H of the
@@ -210,7 +211,14 @@ struct DeviceGuard {
 
 constexpr size_t kSlotBytes = 32u << 20; // staging per slot
 constexpr size_t kZeroCopyMax = 1u << 20; // pinned payloads from this size up are DMA'd even in zero-copy mode
+// DMA mode: pinned payloads below this are packed into the slot's staging by
+// memcpy (one H2D per slot) instead of one hipMemcpyAsync each: a DMA call
+// costs the caller microseconds of CPU, a 4 KiB memcpy a fraction of one
+constexpr size_t kDmaMin = 32u << 10;
 constexpr uint32_t kSlotDescs = 8192;    // descriptors per slot
+// slots whose pieces are all shorter take the direct kernel (one launch, no
+// plan): the balanced range of crc32c_dev_batch_small_async
+constexpr uint32_t kDirectMax = 32u << 10;
 constexpr unsigned kMaxSlots = 4;        // slots in flight per context
 
 struct Piece {
@@ -230,6 +238,7 @@ struct Slot {
 	std::vector<Piece> pieces;
 	std::vector<std::pair<size_t, size_t>> packed; // staging runs filled by memcpy: [lo, hi)
 	size_t used = 0;
+	uint32_t maxlen = 0; // longest piece: the direct kernel takes slots of pieces below kDirectMax
 	bool inflight = false;
 	bool inject_fail = false; // test build: this batch's stream "failed" (PECH_FAULT_ASYNC_STREAM)
 };
@@ -252,6 +261,7 @@ struct crc32c_async {
 	unsigned flags = 0;
 	int efd = -1;
 	bool ready = false; // fully created (destroy drains only then)
+	bool planned_only = false; // PECH_ASYNC_PLANNED=1: every slot on plan + main (A/B measurement)
 	std::vector<Slot *> slots;
 	std::deque<Slot *> inflight; // launch order
 	Slot *cur = nullptr;         // slot being filled
@@ -336,6 +346,7 @@ static void harvest(crc32c_async *a, Slot *s, int err)
 	s->pieces.clear();
 	s->packed.clear();
 	s->used = 0;
+	s->maxlen = 0;
 	s->inflight = false;
 	s->inject_fail = false;
 }
@@ -441,7 +452,8 @@ static int launch_slot(crc32c_async *a)
 		pech_internal_set_err("crc32c_async: injected launch failure (test)");
 		return fail_cur_slot(a, -EIO);
 	}
-	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream);
+	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream,
+				      s->maxlen < kDirectMax && !a->planned_only);
 	if (rc)
 		return fail_cur_slot(a, rc);
 	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), fail_cur_slot(a, -EIO));
@@ -466,6 +478,8 @@ static struct crc32c_async *async_create(unsigned int flags)
 		return nullptr;
 	crc32c_async *a = new crc32c_async();
 	a->flags = flags;
+	const char *pl = getenv("PECH_ASYNC_PLANNED");
+	a->planned_only = pl && pl[0] == '1';
 	if (hipGetDevice(&a->dev) != hipSuccess) {
 		pech_internal_set_err("crc32c_async_create: %s", hipGetErrorString(hipGetLastError()));
 		crc32c_async_destroy(a);
@@ -522,7 +536,7 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 	// kZeroCopyMax) or DMA'd
 	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
 	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len < kZeroCopyMax ? dv : 0;
-	const bool dma = !zc && dv != 0;
+	const bool dma = !zc && dv != 0 && len >= kDmaMin;
 	do {
 		Slot *s = nullptr;
 		int rc = get_slot(a, &s);
@@ -563,6 +577,7 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 		d.len = (uint32_t)piece;
 		d.seed = placed == 0 ? seed : 0u;
 		s->pieces.push_back(Piece{id, (uint32_t)piece});
+		s->maxlen = s->maxlen > piece ? s->maxlen : (uint32_t)piece;
 		++placed;
 		p += piece;
 		left -= piece;

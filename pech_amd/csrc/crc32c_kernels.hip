@@ -745,7 +745,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 #define STEP_ORIG(S) ((S).oz & 0xFFFFFu)
 #define STEP_ZH(S) (((S).oz >> 23) & 15u)
 #define STEP_HEAD(S) (((S).oz >> 20) & 0x7Fu) // row 0's piece is not wholly the buffer's (zoff or zh)
-#define STEP_ZL(S) ((S).oz >> 27)
+#define STEP_ZL(S) ((S).oz & (1u << 27)) // bit 28: STEP_SLOW (direct kernel)
 #define STEP_M(S) ((int64_t)((uint64_t)((S).mp >> 7) * PECH_ROW_BYTES + ((S).mp & 15u)) - (int64_t)((S).mp & 0x70u))
 
 // Ring discipline: row k of a step lives in ring slot k % PECH_U and the
@@ -1378,6 +1378,266 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 	main_body<true, PECH_U_COPY>(lds, cores, lrs, partials, nzs, n, consts, out, rpw_min, deltas);
 }
 
+// ---- direct kernel: small-buffer batches without a plan kernel -------------
+// crc32c_dev_batch_small_async (include/pech_crc32c.h): ONE launch and no
+// workspace.  The batch's positions are split evenly over the waves; each
+// wave walks its positions in steps of 8 (one buffer per group, all of its
+// rows), reading the descriptors itself by scalar loads.  Balanced when the
+// buffers are of similar size -- the caller's contract: every buffer below
+// PECH_SPLIT_ROWS * 128 bytes (32 KiB) -- and correct for any batch (a larger
+// buffer is walked by one group alone).  Heads are masked as in the main
+// kernel; the part of a CRC outside the rows (an unaligned tail, a seed, a
+// buffer inside one 16-byte block) is added at the run's end after a
+// descriptor reload (the slow path, a drain).  Results are stored, not
+// XORed: out[] needs no initialisation.  This saves the plan launch and the
+// main kernel's chunk-scan prologue on the messenger's small payloads.
+#define STEP_SLOW(S) (((S).oz >> 28) & 1u) // the run's buffer has a tail, a seed, or no rows
+
+// The next step of a direct-mode wave: positions [pos, end), interleaved in
+// blocks of 16 (group g takes pos + 2g, then pos + 2g + 1: for buffers laid
+// out back to back every group walks one contiguous 2-buffer range, as the
+// plan kernel's order does), a plain run of up to 8 at the range's end.
+__device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs, const uint32_t *consts,
+					    uint32_t &pos, uint32_t end, uint32_t &ph, uint32_t g8, uint32_t grp)
+{
+	Step S;
+	S.T = 0;
+	S.nmin = 0;
+	S.mp = 0;
+	S.oz = 0;
+	S.nl = 1;
+	S.nu = 0;
+	S.ad = (uint64_t)consts + 16u * g8; // idle groups: valid memory, state ignored
+	S.pos = S.lr = S.rem = 0;
+#ifdef PECH_DEBUG_BOUNDS
+	S.blo = S.ad;
+	S.bhi = S.ad + 16u;
+#endif
+	const uint32_t left = end - pos;
+	if (left == 0) {
+		S.dad = S.ad;
+		return S;
+	}
+	const bool il = ph != 0u || left >= 16u;
+	const uint32_t cnt = il ? 8u : min(left, 8u);
+	// one descriptor per group by scalar loads (wave-uniform addresses)
+	uint32_t alo = 0, ahi = 0, len = 0, seed = 0;
+#pragma unroll
+	for (uint32_t j = 0; j < 8; ++j) {
+		const uint32_t pj = il ? pos + 2u * j + ph : pos + min(j, cnt - 1u);
+		const pech_desc dj = descs[pj];
+		const bool mine = grp == j;
+		alo = mine ? uni((uint32_t)dj.addr) : alo;
+		ahi = mine ? uni((uint32_t)(dj.addr >> 32)) : ahi;
+		len = mine ? uni(dj.len) : len;
+		seed = mine ? uni(dj.seed) : seed;
+	}
+	const uint32_t b = il ? pos + 2u * grp + ph : pos + grp;
+	const bool have = grp < cnt;
+	const uint64_t addr = ((uint64_t)ahi << 32) | alo;
+	const uint32_t rows = have ? pech_core_rows(addr, len) : 0u;
+	const uint64_t end_b = addr + len, ce = end_b & ~(uint64_t)15;
+	const uint32_t t = (uint32_t)(end_b - ce);
+	const uint32_t zt = rows ? pech_core_zt(addr, len, rows) : 0u;
+	const bool slow = have && (t != 0u || seed != 0u || rows == 0u);
+	uint32_t tmax = 0, tmin = 0xFFFFFFFFu, anyslow = 0, dj = 0;
+#pragma unroll
+	for (uint32_t j = 0; j < 8; ++j) {
+		const uint32_t v = lane_value(rows, 8u * j);
+		dj = v > tmax ? j : dj;
+		tmax = max(tmax, v);
+		tmin = v ? min(tmin, v) : tmin;
+		anyslow |= lane_value(slow ? 1u : 0u, 8u * j);
+	}
+	if (tmax) { // idle groups walk the longest buffer's rows (valid memory for the unclamped loop), ignored
+		const uint64_t da = ((uint64_t)lane_value(ahi, 8u * dj) << 32) | lane_value(alo, 8u * dj);
+		S.ad = (da & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + 16u * g8;
+		S.nl = tmax;
+#ifdef PECH_DEBUG_BOUNDS
+		S.blo = S.ad;
+		S.bhi = (da & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + (uint64_t)tmax * PECH_ROW_BYTES;
+#endif
+	}
+	// a step of tiny buffers only (no rows) still runs once, for its slow path
+	S.T = max(tmax, anyslow);
+	S.nmin = tmin == 0xFFFFFFFFu ? 0u : tmin;
+	if (rows) {
+		const uint32_t lb = (uint32_t)addr & (PECH_ROW_BYTES - 1u);
+		S.ad = (addr & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + 16u * g8;
+		S.nl = rows;
+		S.nu = rows;
+		S.oz = head_bits(true, g8, lb) | tail_bits(true, g8, zt);
+#ifdef PECH_DEBUG_BOUNDS
+		S.blo = (addr & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + 16u * (lb >> 4);
+		S.bhi = (addr & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + (uint64_t)rows * PECH_ROW_BYTES;
+#endif
+	}
+	S.oz |= (have ? b : 0u) | (slow ? 1u << 28 : 0u);
+	S.mp = (zt << 4) | t; // m = t - 16 zt: the run ends the core
+	if (il) {
+		pos += ph ? 16u : 0u;
+		ph ^= 1u;
+	} else {
+		pos += cnt;
+	}
+	S.dad = S.ad;
+	return S;
+}
+
+// R(0, bytes [lo, hi) of a 16-byte block): bytes below lo zeroed, the rest
+// moved to the top (leading zeros are free), then the 4-word fold
+// R(0, w0 w1 w2 w3) = A_4(A_4(A_4(A_4(w0) ^ w1) ^ w2) ^ w3)
+__device__ __forceinline__ uint32_t crc_bytes16(const uint32_t *lds, u32x4 v, uint32_t lo, uint32_t hi)
+{
+	uint64_t l = ((uint64_t)v.y << 32) | v.x, h = ((uint64_t)v.w << 32) | v.z;
+	const uint32_t zl = 8u * lo, sh = 8u * (16u - hi);
+	l &= zl >= 64u ? 0ull : ~0ull << zl;
+	h &= zl <= 64u ? ~0ull : ~0ull << (zl - 64u);
+	if (sh >= 64u) {
+		h = sh >= 128u ? 0ull : l << (sh - 64u);
+		l = 0;
+	} else if (sh) {
+		h = (h << sh) | (l >> (64u - sh));
+		l <<= sh;
+	}
+	uint32_t u = adv_tab(lds, L_TAB4, (uint32_t)l) ^ (uint32_t)(l >> 32);
+	u = adv_tab(lds, L_TAB4, u) ^ (uint32_t)h;
+	u = adv_tab(lds, L_TAB4, u) ^ (uint32_t)(h >> 32);
+	return adv_tab(lds, L_TAB4, u);
+}
+
+// Direct mode: fold and shift as finish_run, then add what lies outside the
+// rows (slow path) and store out[b].
+__device__ __forceinline__ void finish_direct(uint32_t *lds, uint32_t g8, uint32_t s0, uint32_t s1, uint32_t s2,
+					      uint32_t s3, const Step &S, const pech_desc *__restrict__ descs,
+					      uint32_t *__restrict__ out)
+{
+	uint32_t u = adv_tab(lds, L_TAB4, s0) ^ s1;
+	u = adv_tab(lds, L_TAB4, u) ^ s2;
+	u = adv_tab(lds, L_TAB4, u) ^ s3;
+	u = adv_tab(lds, L_TAB4, u);
+	u = adv_tab(lds, L_TAB16, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x101, 0xf, 0xf, true);
+	u = adv_tab(lds, L_TAB32, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x102, 0xf, 0xf, true);
+	u = adv_tab(lds, L_TAB64, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x104, 0xf, 0xf, true);
+	const int64_t m = STEP_M(S);
+	const bool lead = g8 == 0u;
+	uint32_t v = 0;
+	if (S.nu != 0u && lead)
+		v = m > 0 ? shift_bytes(lds + L_POWB / 4u, (uint64_t)m, u)
+			  : (m < 0 ? gf2_mulmod(lds[L_XINV / 4u + (uint32_t)(-m)], u) : u);
+	const bool slow = STEP_SLOW(S) != 0u && lead;
+	if (__ballot(slow) != 0ull && slow) { // the rare slow path: its loads wait for the ring too
+		const pech_desc d = descs[STEP_ORIG(S)];
+		const uint64_t end = d.addr + d.len, ce = end & ~(uint64_t)15;
+		const uint32_t lo = ce <= d.addr ? (uint32_t)(d.addr - ce) : 0u, hi = (uint32_t)(end - ce);
+		if (hi > lo) // the tail, or a buffer inside the block at ce
+			v ^= crc_bytes16(lds, *(g_u32x4 *)ce, lo, hi);
+		if (d.seed) // R(s, D) = x^(8|D|) s ^ R(0, D)
+			v ^= d.len ? shift_bytes(lds + L_POWB / 4u, d.len, d.seed) : d.seed;
+	}
+	if ((S.nu != 0u || STEP_SLOW(S) != 0u) && lead)
+		out[STEP_ORIG(S)] = v;
+}
+
+template <uint32_t U>
+__device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__restrict__ descs, uint32_t n,
+					    const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
+{
+	const uint32_t tid = threadIdx.x;
+	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
+	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
+	const uint32_t wave = uni(tid >> 6);
+	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
+	constexpr uint32_t T128 = 1024u / PECH_MAIN_THREADS;
+	constexpr uint32_t NT4 = (PECH_C_TAB1 - PECH_C_TAB4) / 4u;
+	constexpr uint32_t TPT = (NT4 + PECH_MAIN_THREADS - 1u) / PECH_MAIN_THREADS;
+	const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
+	uint32_t t128[T128];
+#pragma unroll
+	for (uint32_t j = 0; j < T128; ++j)
+		t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
+	u32x4 tv[TPT];
+#pragma unroll
+	for (uint32_t k = 0; k < TPT; ++k)
+		tv[k] = c4[min(tid + k * PECH_MAIN_THREADS, NT4 - 1u)];
+	const uint32_t txi = consts[PECH_C_XINV + (tid & 127u)];
+	// the wave's positions: an equal split of the batch
+	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
+	uint32_t pos = (uint32_t)((uint64_t)wglob * n / W), ph = 0;
+	const uint32_t pend = (uint32_t)((uint64_t)(wglob + 1u) * n / W);
+	Step S = plan_direct(descs, consts, pos, pend, ph, g8, grp);
+	u32x4 ring[U];
+	if (S.T)
+		RING_PRIME(S, ring);
+#pragma unroll
+	for (uint32_t j = 0; j < T128; ++j) {
+		const uint32_t w = tid + j * PECH_MAIN_THREADS, k = w >> 8, e = w & 0xFFu;
+		const u32x4 v = (u32x4)(t128[j]);
+		char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+#pragma unroll
+		for (uint32_t q = 0; q < 8u; ++q)
+			*(u32x4 *)(dst + 16u * ((q + w) & 7u)) = v;
+	}
+#pragma unroll
+	for (uint32_t k = 0; k < TPT; ++k)
+		if (tid + k * PECH_MAIN_THREADS < NT4)
+			*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
+	if (tid < 128u)
+		lds[L_XINV / 4u + tid] = txi;
+	__syncthreads(); // tables published; every wave's prime is already in flight
+	while (S.T) {
+		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+		{ // row 0's bytes before the buffer are zeros (as in main_body)
+			const uint32_t sh = STEP_ZOFF(S) ? 128u : 8u * STEP_ZH(S);
+			uint64_t lo = ((uint64_t)ring[0].y << 32) | ring[0].x, hi = ((uint64_t)ring[0].w << 32) | ring[0].z;
+			lo &= sh >= 64u ? 0ull : ~0ull << sh;
+			hi &= sh >= 128u ? 0ull : (sh <= 64u ? ~0ull : ~0ull << (sh - 64u));
+			ring[0] = u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+		}
+		const uint32_t nblk = (S.T + U - 1) / U;
+		const uint32_t last = S.nl - 1u;
+		uint32_t blk = 0;
+		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
+			const uint64_t base = S.ad + (uint64_t)blk * U * PECH_ROW_BYTES;
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i) {
+				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
+				horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
+			}
+		}
+		for (; blk + 1 < nblk; ++blk) {
+			const uint32_t r = blk * U;
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i) {
+				ring[(i + U - 1) % U] = LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
+				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+			}
+		}
+		const uint32_t r = blk * U;
+		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
+		const Step N = plan_direct(descs, consts, pos, pend, ph, g8, grp);
+		horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
+		// branch-free: with no next step the prefetch re-reads this step's last row
+		const bool more = N.T != 0;
+		const Step &L = more ? N : S;
+		const uint32_t lrow0 = more ? 0u : last, lmax = more ? N.nl - 1u : last;
+#pragma unroll
+		for (uint32_t i = 1; i < U; ++i) {
+			ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
+			horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+		}
+		finish_direct(lds, g8, s0, s1, s2, s3, S, descs, out);
+		S = N;
+	}
+}
+
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_direct(
+	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
+	direct_body<PECH_U>(lds, descs, n, consts, out);
+}
+
 // ---- host-side launchers (used by crc32c_api.cpp) -------------------------
 extern "C" hipError_t pech_launch_small(const void *src, uint32_t len, uint32_t seed, const uint32_t *consts,
 					uint32_t *out, uint32_t ticket, hipStream_t stream)
@@ -1419,6 +1679,15 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 		hipExtLaunchKernelGGL(pech_crc32c_main, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop,
 				      0u, (const pech_core *)ws->cores, (const uint32_t *)ws->lrs,
 				      (const uint32_t *)ws->partials, (const uint32_t *)ws->nzs, n, consts, out, rpw_min);
+	return hipGetLastError();
+}
+
+// direct kernel (no plan, no workspace); ev_start/ev_stop as pech_launch_main
+extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, const uint32_t *consts, uint32_t *out,
+					 uint32_t ncu, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)
+{
+	hipExtLaunchKernelGGL(pech_crc32c_direct, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u,
+			      descs, n, consts, out);
 	return hipGetLastError();
 }
 

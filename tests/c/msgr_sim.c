@@ -20,12 +20,14 @@
  *     robin, one eventfd each on the same epoll set.
  * Exit status 0 iff every message verified and none is left pending.
  *
- * Bench mode (bench.py's msgr_async leg for small payloads):
- *   msgr_sim bench <payload bytes> <count> <zerocopy> <passes>
- * submits <count> payloads of crc32c_pages memory per pass (carved from
- * order-11 blocks), flushing every 64, and drains through the eventfd; checks
- * every result of the first pass against the oracle, then prints one JSON
- * line with GiB/s and payloads/s over the timed passes.
+ * Bench mode (bench.py's msgr_async leg):
+ *   msgr_sim bench <payload bytes> <count> <mode> <passes>
+ * mode 0 async DMA, 1 async zero-copy, 2 messenger adapter, 3 host routine
+ * (bench_main): <count> payloads of crc32c_pages memory per pass, flushed
+ * every 64, completed from an epoll loop; checks every result against the
+ * oracle, then prints one JSON line: GiB/s, payloads/s, CPU microseconds per
+ * payload of the calling thread and of the process, submit -> result
+ * latency p50/p99.
  *
  * Build: `make build/msgr_sim` (part of `make all`; gnu89, -Wall -Werror).
  */
@@ -33,11 +35,14 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
+#include <sys/resource.h>
 #include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
+#include "crc32c.h"
 #include "pech_crc32c_async.h"
+#include "pech_crc32c_msgr.h"
 
 /* the test oracle (oracle/crc32c_oracle.c): reference loop, per-piece chain */
 uint32_t oracle_crc32c_pieces(uint32_t crc, const void *data, size_t length, unsigned int piece);
@@ -86,16 +91,9 @@ static unsigned char next_byte(void)
 
 struct bench_slot {
 	uint32_t want, got;
-	int err;
+	int err, done;
+	double t_sub, t_done;
 };
-
-static void bench_done(void *arg, uint32_t crc, int err)
-{
-	struct bench_slot *b = arg;
-
-	b->got = crc;
-	b->err = err;
-}
 
 static double now_s(void)
 {
@@ -105,55 +103,195 @@ static double now_s(void)
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-static int bench_main(unsigned int size, unsigned int count, unsigned int zerocopy, unsigned int passes)
+/* CPU seconds of the calling thread (pech's one OS thread) */
+static double thread_cpu_s(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* CPU seconds of the whole process (HIP runtime threads included) */
+static double process_cpu_s(void)
+{
+	struct rusage ru;
+
+	getrusage(RUSAGE_SELF, &ru);
+	return ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6;
+}
+
+static void bench_done(void *arg, uint32_t crc, int err)
+{
+	struct bench_slot *b = arg;
+
+	b->got = crc;
+	b->err = err;
+	b->done = 1;
+	b->t_done = now_s();
+}
+
+static void bench_release(void *msg)
+{
+	(void)msg; /* the adapter never drops a verified-queue entry here */
+}
+
+static int cmp_double(const void *a, const void *b)
+{
+	const double x = *(const double *)a, y = *(const double *)b;
+
+	return x < y ? -1 : x > y;
+}
+
+/* take verified messages off the adapter's queue (its dispatch loop) */
+static int adapter_dispatch(struct crc32c_msgr_conn *conn, unsigned int *bad)
+{
+	void *msg;
+	uint32_t crc;
+	int rc, n = 0;
+
+	while ((rc = crc32c_msgr_rx_next(conn, &msg, &crc)) != 0) {
+		struct bench_slot *b = msg;
+
+		if (rc < 0)
+			(*bad)++;
+		b->got = crc;
+		b->done = 1;
+		b->t_done = now_s();
+		n++;
+	}
+	return n;
+}
+
+/*
+ * Bench mode: <count> payloads of <size> bytes in crc32c_pages memory per
+ * pass, submitted as a server's read bursts do (flush every 64), completed
+ * from an epoll loop on the context's eventfd (non-blocking complete()
+ * between bursts, epoll_wait at the end).  mode 0: async layer, DMA;
+ * 1: async layer, zero-copy; 2: the messenger adapter (rx_queue / rx_next on
+ * a zero-copy context, its size routing at its default); 3: the drop-in
+ * crc32c() per payload (host routine).  Reports the calling thread's CPU
+ * time per payload (pech's one OS thread), the process's (HIP runtime
+ * threads included) and the submit -> result latency.
+ */
+static int bench_main(unsigned int size, unsigned int count, unsigned int mode, unsigned int passes)
 {
 	const size_t block = (size_t)CRC32C_PAGE_SIZE << 11;
 	const size_t stride = ((size_t)size + 255u) & ~(size_t)255u;
-	const unsigned int per_block = (unsigned int)(block / (stride ? stride : 256u));
-	unsigned int nblocks = (count + per_block - 1) / per_block, i, p, bad = 0;
+	const unsigned int per_block = (unsigned int)(block >= stride ? block / (stride ? stride : 256u) : 0u);
+	const unsigned int order = size > block ? order_for(size) : 11u;
+	const unsigned int nblocks = per_block ? (count + per_block - 1) / per_block : count;
+	unsigned int i, p, bad = 0, k;
 	unsigned char **blocks = calloc(nblocks, sizeof(*blocks));
 	struct bench_slot *slots = calloc(count, sizeof(*slots));
-	struct crc32c_async *a = crc32c_async_create(zerocopy ? CRC32C_ASYNC_ZEROCOPY : CRC32C_ASYNC_DEFAULT);
-	double t0 = 0, t1;
+	double *lat = calloc((size_t)count * passes + 1, sizeof(double));
+	struct crc32c_async *a = NULL;
+	struct crc32c_msgr_conn *conn = NULL;
+	double t0 = 0, c0 = 0, pc0 = 0, t1, c1, pc1;
+	size_t nlat = 0;
+	int ep = -1;
 
-	if (!a || !blocks || !slots || !per_block)
+	if (!blocks || !slots || !lat)
 		return 2;
-	for (i = 0; i < nblocks; i++) {
-		size_t k;
+	if (mode != 3) {
+		struct epoll_event ev;
 
-		blocks[i] = crc32c_pages_alloc(11);
+		a = crc32c_async_create(mode == 0 ? CRC32C_ASYNC_DEFAULT : CRC32C_ASYNC_ZEROCOPY);
+		if (!a)
+			return 2;
+		ep = epoll_create1(0);
+		memset(&ev, 0, sizeof(ev));
+		ev.events = EPOLLIN;
+		if (ep < 0 || epoll_ctl(ep, EPOLL_CTL_ADD, crc32c_async_fd(a), &ev))
+			return 2;
+		if (mode == 2 && !(conn = crc32c_msgr_conn_create(a, count + 1u, NULL, NULL, bench_release)))
+			return 2;
+	}
+	for (i = 0; i < nblocks; i++) {
+		size_t nb = per_block ? block : (size_t)CRC32C_PAGE_SIZE << order;
+
+		blocks[i] = crc32c_pages_alloc(per_block ? 11u : order);
 		if (!blocks[i])
 			return 2;
-		for (k = 0; k < block; k++)
+		for (k = 0; k < nb; k++)
 			blocks[i][k] = next_byte();
 	}
+#define PAYLOAD(i) (per_block ? blocks[(i) / per_block] + (size_t)((i) % per_block) * stride : blocks[i])
 	for (i = 0; i < count; i++)
-		slots[i].want = oracle_crc32c_pieces(0, blocks[i / per_block] + (size_t)(i % per_block) * stride, size,
-						     4096);
+		slots[i].want = oracle_crc32c_pieces(0, PAYLOAD(i), size, 4096);
 	for (p = 0; p <= passes; p++) {
-		if (p == 1)
-			t0 = now_s(); /* pass 0 is the warm-up */
+		unsigned int left = count;
+
+		if (p == 1) { /* pass 0 is the warm-up */
+			t0 = now_s();
+			c0 = thread_cpu_s();
+			pc0 = process_cpu_s();
+		}
+		for (i = 0; i < count; i++)
+			slots[i].done = 0;
 		for (i = 0; i < count; i++) {
-			if (crc32c_async_submit(a, blocks[i / per_block] + (size_t)(i % per_block) * stride, size, 0,
-						bench_done, &slots[i]))
+			struct bench_slot *b = &slots[i];
+
+			b->t_sub = now_s();
+			if (mode == 3) {
+				b->got = crc32c(0, PAYLOAD(i), size);
+				b->done = 1;
+				b->t_done = now_s();
+				left--;
+				continue;
+			}
+			if (mode == 2) {
+				if (crc32c_msgr_rx_queue(conn, b, PAYLOAD(i), size, 1, b->want))
+					return 2;
+			} else if (crc32c_async_submit(a, PAYLOAD(i), size, 0, bench_done, b)) {
 				return 2;
-			if (i % 64 == 63 && crc32c_async_flush(a))
+			}
+			if (i % 64 == 63) { /* end of a read burst: flush, complete without blocking */
+				if (crc32c_async_flush(a) || crc32c_async_complete(a) < 0)
+					return 2;
+				if (mode == 2)
+					adapter_dispatch(conn, &bad);
+			}
+		}
+		if (a && crc32c_async_flush(a))
+			return 2;
+		for (;;) { /* the event loop until every result is in */
+			struct epoll_event ev;
+
+			if (mode == 2)
+				adapter_dispatch(conn, &bad);
+			for (left = 0, i = 0; i < count; i++)
+				left += !slots[i].done;
+			if (!left)
+				break;
+			if (epoll_wait(ep, &ev, 1, 10000) <= 0)
+				return 3;
+			if (crc32c_async_complete(a) < 0)
 				return 2;
 		}
-		if (crc32c_async_drain(a))
-			return 2;
-		if (p == 0)
-			for (i = 0; i < count; i++)
-				bad += slots[i].err || slots[i].got != slots[i].want;
+		for (i = 0; i < count; i++) {
+			bad += slots[i].err || slots[i].got != slots[i].want;
+			if (p > 0)
+				lat[nlat++] = slots[i].t_done - slots[i].t_sub;
+		}
 	}
+#undef PAYLOAD
 	t1 = now_s();
-	printf("{\"payload_bytes\": %u, \"payloads\": %u, \"passes\": %u, \"zerocopy\": %u, \"bad\": %u, "
-	       "\"GiBps\": %.3f, \"payloads_per_s\": %.0f}\n",
-	       size, count, passes, zerocopy, bad, (double)size * count * passes / (t1 - t0) / (1u << 30),
-	       (double)count * passes / (t1 - t0));
-	crc32c_async_destroy(a);
+	c1 = thread_cpu_s();
+	pc1 = process_cpu_s();
+	qsort(lat, nlat, sizeof(double), cmp_double);
+	printf("{\"payload_bytes\": %u, \"payloads\": %u, \"passes\": %u, \"mode\": \"%s\", \"bad\": %u, "
+	       "\"GiBps\": %.3f, \"payloads_per_s\": %.0f, \"thread_cpu_us_per_payload\": %.3f, "
+	       "\"process_cpu_us_per_payload\": %.3f, \"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f}\n",
+	       size, count, passes, mode == 0 ? "async-dma" : mode == 1 ? "async-zerocopy" : mode == 2 ? "adapter" : "host",
+	       bad, (double)size * count * passes / (t1 - t0) / (1u << 30), (double)count * passes / (t1 - t0),
+	       (c1 - c0) / ((double)count * passes) * 1e6, (pc1 - pc0) / ((double)count * passes) * 1e6,
+	       nlat ? lat[nlat / 2] * 1e6 : 0.0, nlat ? lat[(size_t)(nlat * 0.99)] * 1e6 : 0.0);
+	crc32c_msgr_conn_destroy(conn);
+	if (a)
+		crc32c_async_destroy(a);
 	for (i = 0; i < nblocks; i++)
-		crc32c_pages_free(blocks[i], 11);
+		crc32c_pages_free(blocks[i], per_block ? 11u : order);
 	crc32c_pages_trim();
 	return bad ? 1 : 0;
 }

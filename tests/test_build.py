@@ -41,7 +41,7 @@ def kernel_body(asm, name):
 
 
 @pytest.mark.parametrize("kernel", ["pech_crc32c_plan", "pech_crc32c_main", "pech_crc32c_plan_copy",
-                                    "pech_crc32c_main_copy", "pech_crc32c_small"])
+                                    "pech_crc32c_main_copy", "pech_crc32c_small", "pech_crc32c_direct"])
 def test_no_calls_no_scratch(device_asm, kernel):
     asm, _ = device_asm
     body = kernel_body(asm, kernel)
@@ -49,7 +49,7 @@ def test_no_calls_no_scratch(device_asm, kernel):
     assert "scratch_" not in body and "buffer_store_dword" not in body, "register spill"
 
 
-@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy"])
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct"])
 def test_main_kernel_register_budget(device_asm, kernel):
     _, remarks = device_asm
     m = re.search(r"Function Name: %s \[.*?VGPRs: (\d+).*?ScratchSize \[bytes/lane\]: (\d+)" % kernel, remarks,
@@ -84,7 +84,8 @@ def _blocks(body):
     return out
 
 
-def test_row_loops_never_drain_the_ring(device_asm, kernel="pech_crc32c_main"):
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_direct"])
+def test_row_loops_never_drain_the_ring(device_asm, kernel):
     """The row loops (basic blocks with a full block of Horner steps and
     their prefetch loads) keep PECH_U-1 loads in flight across the back
     edge: no vmcnt(0) and no ring-register copies (which is what a ring

@@ -476,23 +476,25 @@ def test_concurrent_streams_explicit_workspaces(torch_dev, P):
 
 
 def test_graph_capture_and_replay(torch_dev, P):
-    # the device batch enqueues no host sync / allocation: capturable
+    # the device batch enqueues no host sync / allocation: capturable with
+    # its own workspace; the internal workspace is refused inside a capture
+    # (a replay would use it outside the library's stream ordering)
     torch, dev = torch_dev
     n, L = 256, 65536
     buf = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev)
     offs = np.arange(n) * L
     descs = P.make_descs([buf.data_ptr() + int(o) for o in offs], [L] * n, device=dev)
     out = torch.zeros(n, dtype=torch.int32, device=dev)
-    from pech_amd import _lib
-
-    assert _lib.lib().crc32c_dev_reserve(n) == 0
+    ws = torch.empty(P.workspace_bytes(n), dtype=torch.uint8, device=dev)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        P.dev_batch_async(descs, out, stream=s)  # warm-up outside capture
+        P.dev_batch_ws_async(descs, out, ws, stream=s)  # warm-up outside capture
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        P.dev_batch_async(descs, out, stream=s)
+        with pytest.raises(P.Crc32cError, match="graph"):
+            P.dev_batch_async(descs, out, stream=s)
+        P.dev_batch_ws_async(descs, out, ws, stream=s)
     out.zero_()
     g.replay()
     torch.cuda.synchronize()
