@@ -81,7 +81,7 @@ void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c);
  * free the adapter. */
 void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c);
 
-/* Payloads of at most `bytes` (default 16 KiB, or PECH_CRC32C_MSGR_HOST_MAX
+/* Payloads of at most `bytes` (default 8 KiB, or PECH_CRC32C_MSGR_HOST_MAX
  * in the environment) are checksummed at once on the host instead of the
  * GPU: below the crossover the host routine costs less CPU time than the
  * GPU round trip.  Process-wide; returns the previous

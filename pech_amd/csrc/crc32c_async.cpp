@@ -37,6 +37,7 @@
 
 #include <errno.h>
 #include <stdlib.h>
+#include <time.h>
 #include <string.h>
 #include <sys/eventfd.h>
 #include <unistd.h>
@@ -190,21 +191,34 @@ static uint64_t pinned_dev_addr(const void *p, size_t len)
 // async contexts
 namespace {
 
-// Every entry point runs on its context's device and restores the caller's:
-// one thread can drive one context per GPU without
-// tracking the current device itself.
+// Every entry point that calls HIP runs on its context's device and restores
+// the caller's: one thread can drive one context per GPU (SURVEY 7 step 7,
+// 8e) without tracking the current device itself.  Lazy: the common submit
+// (a descriptor into the open slot) and complete (slots already finished)
+// make no HIP call at all, and a HIP call costs the caller's thread more than
+// the descriptor does (tools/c/launch_cost.c).
 struct DeviceGuard {
-	int prev = -1;
-	bool ok = false;
-	explicit DeviceGuard(int dev)
+	int dev, prev = -1;
+	bool tried = false, ok = false, changed = false;
+	explicit DeviceGuard(int d, bool now = true) : dev(d)
 	{
+		if (now)
+			ensure();
+	}
+	bool ensure()
+	{
+		if (tried)
+			return ok;
+		tried = true;
 		if (hipGetDevice(&prev) != hipSuccess)
-			return;
-		ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+			return false;
+		changed = prev != dev;
+		ok = !changed || hipSetDevice(dev) == hipSuccess;
+		return ok;
 	}
 	~DeviceGuard()
 	{
-		if (ok && prev >= 0)
+		if (ok && changed)
 			(void)hipSetDevice(prev);
 	}
 };
@@ -220,6 +234,7 @@ constexpr uint32_t kSlotDescs = 8192;    // descriptors per slot
 // plan): the balanced range of crc32c_dev_batch_small_async
 constexpr uint32_t kDirectMax = 32u << 10;
 constexpr unsigned kMaxSlots = 4;        // slots in flight per context
+constexpr uint64_t kQueryAfterNs = 1000000; // complete(): a stream is queried once its batch is this old
 
 struct Piece {
 	uint64_t item; // submission id
@@ -241,7 +256,15 @@ struct Slot {
 	uint32_t maxlen = 0; // longest piece: the direct kernel takes slots of pieces below kDirectMax
 	bool inflight = false;
 	bool inject_fail = false; // test build: this batch's stream "failed" (PECH_FAULT_ASYNC_STREAM)
+	uint64_t t_launch = 0;    // mono_ns() at launch
 };
+
+static inline uint64_t mono_ns()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 
 struct Item {
 	crc32c_done_fn done;
@@ -352,7 +375,7 @@ static void harvest(crc32c_async *a, Slot *s, int err)
 }
 
 // Harvest finished slots (blocking on the oldest when `wait`), in order.
-static int reap(crc32c_async *a, bool wait_oldest)
+static int reap(crc32c_async *a, bool wait_oldest, DeviceGuard *dg = nullptr)
 {
 	while (!a->inflight.empty()) {
 		Slot *s = a->inflight.front();
@@ -365,7 +388,12 @@ static int reap(crc32c_async *a, bool wait_oldest)
 				// the host function runs on the runtime's thread: a moment
 			}
 		} else if (!s->finished.load(std::memory_order_acquire)) {
-			// a failed stream never runs its host function: ask the stream
+			// a failed stream never runs its host function: ask the stream,
+			// once the batch has had kQueryAfterNs to finish (complete() is
+			// called from the fd and from a timer; a query costs the caller's
+			// thread microseconds, and the fd normally fires first)
+			if (mono_ns() - s->t_launch < kQueryAfterNs || (dg && !dg->ensure()))
+				return 0;
 			q = hipStreamQuery(s->stream);
 			if (q == hipSuccess && s->inject_fail)
 				q = hipErrorLaunchFailure; // test build: as a failed stream reports itself
@@ -463,6 +491,7 @@ static int launch_slot(crc32c_async *a)
 	if (!s->inject_fail)
 		TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_cur_slot(a, -EIO));
 	s->inflight = true;
+	s->t_launch = mono_ns();
 	a->inflight.push_back(s);
 	a->cur = nullptr;
 	return 0;
@@ -513,8 +542,17 @@ extern "C" int crc32c_async_fd(const struct crc32c_async *a)
 static int async_submit(struct crc32c_async *a, const void *buf, unsigned int len, uint32_t seed,
 			crc32c_done_fn done, void *arg)
 {
-	DeviceGuard dg(a->dev);
-	if (!dg.ok) {
+	// one registry lookup: pinned pages are read in place (zero-copy, below
+	// kZeroCopyMax) or DMA'd
+	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
+	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len < kZeroCopyMax ? dv : 0;
+	const bool dma = !zc && dv != 0 && len >= kDmaMin;
+	// the common case needs no HIP call: one descriptor into the open slot,
+	// which it does not fill
+	const Slot *c = a->cur;
+	const bool quiet = c && !dma && c->pieces.size() + 1u < kSlotDescs && (zc || c->used + len + 512u < kSlotBytes);
+	DeviceGuard dg(a->dev, !quiet);
+	if (!quiet && !dg.ok) {
 		pech_internal_set_err("crc32c_async_submit: cannot select device %d", a->dev);
 		return -ENODEV;
 	}
@@ -532,11 +570,6 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 		it.cancelled = true;
 		return rc;
 	};
-	// one registry lookup: pinned pages are read in place (zero-copy, below
-	// kZeroCopyMax) or DMA'd
-	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
-	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len < kZeroCopyMax ? dv : 0;
-	const bool dma = !zc && dv != 0 && len >= kDmaMin;
 	do {
 		Slot *s = nullptr;
 		int rc = get_slot(a, &s);
@@ -648,11 +681,11 @@ extern "C" int crc32c_async_complete(struct crc32c_async *a)
 	if (!a)
 		return -EINVAL;
 	const int rc = on_lib_stack([&] {
-		DeviceGuard dg(a->dev);
 		uint64_t cnt;
 		while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
 		}
-		return reap(a, false);
+		DeviceGuard dg(a->dev, false); // reap() selects it before a stream query
+		return reap(a, false, &dg);
 	});
 	const int ran = run_callbacks(a);
 	return rc ? rc : ran;

@@ -29,7 +29,7 @@
 #define PECH_HIDDEN __attribute__((visibility("hidden")))
 PECH_HIDDEN uint32_t pech_cpu_crc32c(uint32_t crc, const void *data, size_t n);
 
-#define PECH_MSGR_HOST_MAX_DEFAULT (16u << 10)
+#define PECH_MSGR_HOST_MAX_DEFAULT (8u << 10) /* profiles/r03/msgr_cutoff.txt */
 #define TX_BUCKETS 64u /* per connection, chained by msg address */
 
 enum { ST_WAIT, ST_DONE };

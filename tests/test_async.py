@@ -167,7 +167,7 @@ def test_msgr_connection_state_machine(mode, corrupt, host_max):
     exe = os.path.join(REPO, "build", "msgr_conn_sim")
     assert os.path.exists(exe), "build/msgr_conn_sim is built by `make`"
     # host_max: the adapter's size routing (crc32c_msgr_set_host_max): by
-    # default payloads <= 16 KiB are checksummed on the host and the larger
+    # default payloads <= 8 KiB are checksummed on the host and the larger
     # ones on the GPU; "0" sends every checked payload to the GPU
     env = dict(os.environ)
     if host_max is not None:

@@ -1,7 +1,8 @@
 /*
  * Host CPU cost of the HIP calls one async-layer slot makes (GPU box):
- * thread CPU microseconds per call of each, issued back to back on one
- * stream with a synchronize every 64 calls (a flush's worth), so the
+ * wall microseconds inside each call (call_us; the calls do not block), issued
+ * back to back on one stream with a synchronize every 64 calls (a flush's
+ * worth; the _incl_sync figures add the spin of that wait), so the
  * messenger's per-payload cost can be split into its launch parts.
  *   build/launch_cost [iters]
  */
@@ -54,7 +55,9 @@ int main(int argc, char **argv)
 	uint8_t *d_buf;
 	const char *names[] = {"small_async(64 descs)", "dev_batch_async(64 descs, plan+main)",
 			       "memcpy D2H 256 B", "memcpy H2D 1 KiB", "hipLaunchHostFunc(noop)",
-			       "small_async on mapped host descs + out", "hipEventRecord"};
+			       "small_async on mapped host descs + out", "hipEventRecord", "hipGetDevice",
+			       "hipSetDevice(same)", "hipStreamQuery(idle)"};
+	int dev;
 	hipEvent_t ev;
 	int k, i;
 
@@ -76,8 +79,8 @@ int main(int argc, char **argv)
 	}
 	CHECK(hipMemcpy(d_desc, h_desc, N_DESC * sizeof(*d_desc), hipMemcpyHostToDevice));
 	CHECK(crc32c_dev_reserve(N_DESC));
-	for (k = 0; k < 7; k++) {
-		double c0 = 0, w0 = 0;
+	for (k = 0; k < 10; k++) {
+		double c0 = 0, w0 = 0, in_call = 0;
 		int pass;
 
 		for (pass = 0; pass < 2; pass++) { /* pass 0: warm-up */
@@ -86,8 +89,11 @@ int main(int argc, char **argv)
 			if (pass) {
 				c0 = thread_cpu_s();
 				w0 = wall_s();
+				in_call = 0;
 			}
 			for (i = 0; i < n; i++) {
+				const double a = wall_s();
+
 				switch (k) {
 				case 0: CHECK(crc32c_dev_batch_small_async(d_desc, d_out, N_DESC, st)); break;
 				case 1: CHECK(crc32c_dev_batch_async(d_desc, d_out, N_DESC, st)); break;
@@ -96,13 +102,18 @@ int main(int argc, char **argv)
 				case 4: CHECK(hipLaunchHostFunc(st, noop, NULL)); break;
 				case 5: CHECK(crc32c_dev_batch_small_async(m_desc, m_out, N_DESC, st)); break;
 				case 6: CHECK(hipEventRecord(ev, st)); break;
+				case 7: CHECK(hipGetDevice(&dev)); break;
+				case 8: CHECK(hipSetDevice(0)); break;
+				case 9: CHECK(hipStreamQuery(st)); break;
 				}
+				in_call += wall_s() - a;
 				if (i % 64 == 63)
 					CHECK(hipStreamSynchronize(st));
 			}
 			CHECK(hipStreamSynchronize(st));
 		}
-		printf("{\"call\": \"%s\", \"thread_cpu_us\": %.3f, \"wall_us\": %.3f}\n", names[k],
+		printf("{\"call\": \"%s\", \"call_us\": %.3f, \"thread_cpu_us_incl_sync\": %.3f, "
+		       "\"wall_us_incl_sync\": %.3f}\n", names[k], in_call / iters * 1e6,
 		       (thread_cpu_s() - c0) / iters * 1e6, (wall_s() - w0) / iters * 1e6);
 	}
 	for (i = 0; i < N_DESC; i++)
