@@ -1385,13 +1385,29 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 // rows), reading the descriptors itself by scalar loads.  Balanced when the
 // buffers are of similar size -- the caller's contract: every buffer below
 // PECH_SPLIT_ROWS * 128 bytes (32 KiB) -- and correct for any batch (a larger
-// buffer is walked by one group alone).  Heads are masked as in the main
-// kernel; the part of a CRC outside the rows (an unaligned tail, a seed, a
-// buffer inside one 16-byte block) is added at the run's end after a
-// descriptor reload (the slow path, a drain).  Results are stored, not
-// XORed: out[] needs no initialisation.  This saves the plan launch and the
-// main kernel's chunk-scan prologue on the messenger's small payloads.
-#define STEP_SLOW(S) (((S).oz >> 28) & 1u) // the run's buffer has a tail, a seed, or no rows
+// buffer is walked by one group alone).  A buffer's rows cover ALL of its
+// bytes: row 0's bytes before it are masked as in the main kernel (head), the
+// last row's bytes after it are masked too (tail: piece by piece), and the
+// trailing zeros are undone by one x^(-8 trail) multiply, trail < 128 -- no
+// tail block load: an unaligned end costs nothing beyond the row it shares.
+// Only a seed (or an empty buffer) takes the slow path, a descriptor reload
+// at the run's end.  Results are stored, not XORed: out[] needs no
+// initialisation.  This saves the plan launch and the main kernel's
+// chunk-scan prologue on the messenger's small payloads.
+#define STEP_SLOW(S) (((S).oz >> 28) & 1u) // the run's buffer has a seed, or no bytes
+#define DSTEP_TRAIL(S) ((S).mp & 0x7Fu)     // zero bytes after the buffer in its last row
+#define DSTEP_KB(S) (((S).mp >> 8) & 31u)    // bytes of the lane's piece kept in the last row
+
+// Direct mode: the last row's piece keeps its bytes below DSTEP_KB (64-bit
+// halves, as the head mask)
+__device__ __forceinline__ u32x4 tail_keep(const Step &S, uint32_t row, u32x4 v)
+{
+	const uint32_t kb = row == S.nu - 1u ? DSTEP_KB(S) : 16u;
+	uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+	lo &= kb >= 8u ? ~0ull : (1ull << (8u * kb)) - 1ull;
+	hi &= kb >= 16u ? ~0ull : (kb <= 8u ? 0ull : (1ull << (8u * (kb - 8u))) - 1ull);
+	return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
 
 // The next step of a direct-mode wave: positions [pos, end), interleaved in
 // blocks of 16 (group g takes pos + 2g, then pos + 2g + 1: for buffers laid
@@ -1435,11 +1451,9 @@ __device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs,
 	const uint32_t b = il ? pos + 2u * grp + ph : pos + grp;
 	const bool have = grp < cnt;
 	const uint64_t addr = ((uint64_t)ahi << 32) | alo;
-	const uint32_t rows = have ? pech_core_rows(addr, len) : 0u;
-	const uint64_t end_b = addr + len, ce = end_b & ~(uint64_t)15;
-	const uint32_t t = (uint32_t)(end_b - ce);
-	const uint32_t zt = rows ? pech_core_zt(addr, len, rows) : 0u;
-	const bool slow = have && (t != 0u || seed != 0u || rows == 0u);
+	const uint32_t lb = alo & (PECH_ROW_BYTES - 1u);
+	const uint32_t rows = have ? (uint32_t)(((uint64_t)lb + len + PECH_ROW_BYTES - 1u) >> 7) : 0u;
+	const bool slow = have && (seed != 0u || rows == 0u);
 	uint32_t tmax = 0, tmin = 0xFFFFFFFFu, anyslow = 0, dj = 0;
 #pragma unroll
 	for (uint32_t j = 0; j < 8; ++j) {
@@ -1462,18 +1476,19 @@ __device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs,
 	S.T = max(tmax, anyslow);
 	S.nmin = tmin == 0xFFFFFFFFu ? 0u : tmin;
 	if (rows) {
-		const uint32_t lb = (uint32_t)addr & (PECH_ROW_BYTES - 1u);
 		S.ad = (addr & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + 16u * g8;
 		S.nl = rows;
 		S.nu = rows;
-		S.oz = head_bits(true, g8, lb) | tail_bits(true, g8, zt);
+		S.oz = head_bits(true, g8, lb);
+		// mod 2^32: the true values are < 128 and in (0, 128]
+		const uint32_t e = lb + len - (rows - 1u) * PECH_ROW_BYTES;
+		S.mp = (rows * PECH_ROW_BYTES - lb - len) | (min(e - min(e, 16u * g8), 16u) << 8);
 #ifdef PECH_DEBUG_BOUNDS
 		S.blo = (addr & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + 16u * (lb >> 4);
 		S.bhi = (addr & ~(uint64_t)(PECH_ROW_BYTES - 1u)) + (uint64_t)rows * PECH_ROW_BYTES;
 #endif
 	}
 	S.oz |= (have ? b : 0u) | (slow ? 1u << 28 : 0u);
-	S.mp = (zt << 4) | t; // m = t - 16 zt: the run ends the core
 	if (il) {
 		pos += ph ? 16u : 0u;
 		ph ^= 1u;
@@ -1484,30 +1499,8 @@ __device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs,
 	return S;
 }
 
-// R(0, bytes [lo, hi) of a 16-byte block): bytes below lo zeroed, the rest
-// moved to the top (leading zeros are free), then the 4-word fold
-// R(0, w0 w1 w2 w3) = A_4(A_4(A_4(A_4(w0) ^ w1) ^ w2) ^ w3)
-__device__ __forceinline__ uint32_t crc_bytes16(const uint32_t *lds, u32x4 v, uint32_t lo, uint32_t hi)
-{
-	uint64_t l = ((uint64_t)v.y << 32) | v.x, h = ((uint64_t)v.w << 32) | v.z;
-	const uint32_t zl = 8u * lo, sh = 8u * (16u - hi);
-	l &= zl >= 64u ? 0ull : ~0ull << zl;
-	h &= zl <= 64u ? ~0ull : ~0ull << (zl - 64u);
-	if (sh >= 64u) {
-		h = sh >= 128u ? 0ull : l << (sh - 64u);
-		l = 0;
-	} else if (sh) {
-		h = (h << sh) | (l >> (64u - sh));
-		l <<= sh;
-	}
-	uint32_t u = adv_tab(lds, L_TAB4, (uint32_t)l) ^ (uint32_t)(l >> 32);
-	u = adv_tab(lds, L_TAB4, u) ^ (uint32_t)h;
-	u = adv_tab(lds, L_TAB4, u) ^ (uint32_t)(h >> 32);
-	return adv_tab(lds, L_TAB4, u);
-}
-
-// Direct mode: fold and shift as finish_run, then add what lies outside the
-// rows (slow path) and store out[b].
+// Direct mode: fold as finish_run, undo the trailing zeros, add the seed's
+// term (slow path) and store out[b].
 __device__ __forceinline__ void finish_direct(uint32_t *lds, uint32_t g8, uint32_t s0, uint32_t s1, uint32_t s2,
 					      uint32_t s3, const Step &S, const pech_desc *__restrict__ descs,
 					      uint32_t *__restrict__ out)
@@ -1519,19 +1512,15 @@ __device__ __forceinline__ void finish_direct(uint32_t *lds, uint32_t g8, uint32
 	u = adv_tab(lds, L_TAB16, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x101, 0xf, 0xf, true);
 	u = adv_tab(lds, L_TAB32, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x102, 0xf, 0xf, true);
 	u = adv_tab(lds, L_TAB64, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x104, 0xf, 0xf, true);
-	const int64_t m = STEP_M(S);
 	const bool lead = g8 == 0u;
 	uint32_t v = 0;
-	if (S.nu != 0u && lead)
-		v = m > 0 ? shift_bytes(lds + L_POWB / 4u, (uint64_t)m, u)
-			  : (m < 0 ? gf2_mulmod(lds[L_XINV / 4u + (uint32_t)(-m)], u) : u);
+	if (S.nu != 0u && lead) {
+		const uint32_t tr = DSTEP_TRAIL(S);
+		v = tr ? gf2_mulmod(lds[L_XINV / 4u + tr], u) : u;
+	}
 	const bool slow = STEP_SLOW(S) != 0u && lead;
-	if (__ballot(slow) != 0ull && slow) { // the rare slow path: its loads wait for the ring too
+	if (__ballot(slow) != 0ull && slow) { // the rare slow path: its load waits for the ring too
 		const pech_desc d = descs[STEP_ORIG(S)];
-		const uint64_t end = d.addr + d.len, ce = end & ~(uint64_t)15;
-		const uint32_t lo = ce <= d.addr ? (uint32_t)(d.addr - ce) : 0u, hi = (uint32_t)(end - ce);
-		if (hi > lo) // the tail, or a buffer inside the block at ce
-			v ^= crc_bytes16(lds, *(g_u32x4 *)ce, lo, hi);
 		if (d.seed) // R(s, D) = x^(8|D|) s ^ R(0, D)
 			v ^= d.len ? shift_bytes(lds + L_POWB / 4u, d.len, d.seed) : d.seed;
 	}
@@ -1610,13 +1599,16 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] = LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
-				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+				horner_row_pred(lds, lreg, tail_keep(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 			}
 		}
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
 		const Step N = plan_direct(descs, consts, pos, pend, ph, g8, grp);
-		horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
+		// the last block's rows past every group's run (S.T, wave-uniform)
+		// are skipped by a scalar branch: their loads keep the ring's order
+		if (r < S.T)
+			horner_row_pred(lds, lreg, tail_keep(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
 		// branch-free: with no next step the prefetch re-reads this step's last row
 		const bool more = N.T != 0;
 		const Step &L = more ? N : S;
@@ -1624,7 +1616,8 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 #pragma unroll
 		for (uint32_t i = 1; i < U; ++i) {
 			ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
-			horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+			if (r + i < S.T)
+				horner_row_pred(lds, lreg, tail_keep(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 		}
 		finish_direct(lds, g8, s0, s1, s2, s3, S, descs, out);
 		S = N;

@@ -1,6 +1,7 @@
 """The bounds-checked kernel build (build/lib_dbg.so, -DPECH_DEBUG_BOUNDS,
 built by `make`) on C4- and C2-shaped batches with unaligned starts and
-ragged ends: every ring load is checked against its buffer's core on the
+ragged ends: every ring load (plan + main kernels, and the direct kernel of the
+small-buffer API) is checked against its buffer's rows on the
 GPU (a violation prints "PECH OOB" and is redirected instead of faulting),
 and every result must still equal the oracle.  Runs in a subprocess so the
 release library stays the one this test process loads."""
@@ -37,7 +38,11 @@ seeds = rng.integers(0, 1 << 32, lens.size, dtype=np.uint64)
 buf = torch.from_numpy(host).to(dev)
 descs = P.make_descs(buf.data_ptr() + offs, lens, seeds, device=dev)
 out = torch.zeros(lens.size, dtype=torch.int32, device=dev)
-P.dev_batch_async(descs, out)
+if sys.argv[3] == "small":  # the direct kernel (no plan), C2 shapes and the over-contract C4 mix
+    out.fill_(-1)
+    P.dev_batch_small_async(descs, out)
+else:
+    P.dev_batch_async(descs, out)
 torch.cuda.synchronize()
 got = out.cpu().numpy().view(np.uint32)
 assert np.array_equal(got, O.crcs(host, offs, lens, seeds)), "parity"
@@ -45,12 +50,13 @@ print("ok", lens.size, int(lens.sum()))
 """
 
 
-@pytest.mark.parametrize("seed,shape", [(1, "c4"), (2, "c2"), (3, "c4")])
-def test_bounds_checked_build(seed, shape):
+@pytest.mark.parametrize("seed,shape,api", [(1, "c4", "planned"), (2, "c2", "planned"), (3, "c4", "planned"),
+                                            (4, "c2", "small"), (5, "c4", "small")])
+def test_bounds_checked_build(seed, shape, api):
     lib = os.path.join(REPO, "build", "lib_dbg.so")
     assert os.path.exists(lib), "build/lib_dbg.so is built by `make`"
     env = dict(os.environ, PECH_CRC32C_LIB=lib)
-    r = subprocess.run([sys.executable, "-c", SCRIPT, str(seed), shape], cwd=REPO, env=env, capture_output=True,
+    r = subprocess.run([sys.executable, "-c", SCRIPT, str(seed), shape, api], cwd=REPO, env=env, capture_output=True,
                        timeout=300)
     out = r.stdout.decode() + r.stderr.decode()
     assert "PECH OOB" not in out, out[-3000:]
