@@ -1138,9 +1138,8 @@ int crc32c_test_inject(int site, int countdown)
 	g_fault[site].store(countdown);
 	return 0;
 }
-#endif
 
-// Read-only diagnostics (tests/test_cpu_path.py): they change no state.
+// Read-only diagnostics (tests/test_cpu_path.py), also test build only.
 // the host routine itself: variant 0 = the one crc32c() uses (SSE4.2 when
 // the CPU has it), 1 = portable slice-by-8
 uint32_t crc32c_test_cpu(uint32_t crc, const void *data, size_t n, int variant)
@@ -1158,5 +1157,6 @@ int crc32c_test_stack_switch(void)
 {
 	return on_lib_stack([] { return pech_on_lib_stack(); });
 }
+#endif
 
 } // extern "C"

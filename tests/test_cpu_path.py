@@ -20,14 +20,23 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KAT = json.load(open(os.path.join(REPO, "tests", "golden", "kat.json")))
 
 
-def L():
-    from pech_amd import _lib
+_TEST_LIB = None
 
-    lib = _lib.lib()
+
+def L():
+    """build/lib_test.so: the release objects plus the test hooks
+    (-DPECH_TEST_HOOKS); the release library exports none of them."""
+    global _TEST_LIB
+    if _TEST_LIB is not None:
+        return _TEST_LIB
+    path = os.path.join(REPO, "build", "lib_test.so")
+    assert os.path.exists(path), "build/lib_test.so is built by `make`"
+    lib = ctypes.CDLL(path)
     lib.crc32c_test_cpu.restype = ctypes.c_uint32
     lib.crc32c_test_cpu.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     lib.crc32c_test_cpu_has_sse42.restype = ctypes.c_int
     lib.crc32c_test_stack_switch.restype = ctypes.c_int
+    _TEST_LIB = lib
     return lib
 
 

@@ -294,7 +294,7 @@ def test_release_library_has_no_fault_hook():
     # failure injection is not exported by the release library
     out = subprocess.check_output(["nm", "-D", "--defined-only", os.path.join(REPO, "pech_amd", "libpech_crc32c.so")],
                                   text=True)
-    assert "crc32c_test_inject" not in out
+    assert "crc32c_test_" not in out  # no test hook at all (inject, cpu variants, stack switch)
     if os.path.exists(TEST_LIB):
         assert "crc32c_test_inject" in subprocess.check_output(["nm", "-D", "--defined-only", TEST_LIB], text=True)
 
