@@ -603,6 +603,134 @@ __global__ __launch_bounds__(1024, 1) void k_tiles(const uint8_t *p, uint8_t *q,
 		out[w] = 1u;
 }
 
+// The in-flight address window (round 3): the grid copy with one float4 per
+// thread runs at 335 us, with 4 / 16 per thread at 366 / 401, i.e. as slow as
+// the static persistent copy -- the wider the set of addresses in flight at
+// once, the slower, with no store waits in any of them.  Persistent tiles
+// (k_tiles) should give the grid's narrow window, but waves drift apart
+// (oldest-first issue), so here every wave runs the same number of tile
+// steps with a workgroup barrier after each: a CU's 16 waves stay on 16
+// adjacent tiles and the chip on a window of about W tiles.  144 KiB of LDS
+// as the CRC kernel, so one workgroup per CU.
+template <bool COPY, uint32_t TR, bool SYNC>
+__global__ __launch_bounds__(1024, 1) void k_tiles_sync(const uint8_t *p, uint8_t *q, uint32_t R, uint32_t *out)
+{
+	__shared__ uint32_t pad[36 * 1024];
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	constexpr uint32_t PER = TR / 8u;
+	static_assert(PER % D == 0, "tile slice: whole ring blocks");
+	pad[threadIdx.x] = lane;
+	const uint32_t ntiles = (R + TR - 1u) / TR, steps = (ntiles + W - 1u) / W;
+	u32x4 acc = (u32x4)(0u), ring[D];
+	for (uint32_t k = 0; k < steps; ++k) {
+		const uint32_t t = k * W + w;
+		if (t < ntiles) {
+			const uint32_t row0 = t * TR + grp * PER;
+			for (uint32_t r = 0; r < PER; r += D) {
+#pragma unroll
+				for (int i = 0; i < D; ++i)
+					ring[i] = ld(p, min(row0 + r + i, R - 1u), g8);
+#pragma unroll
+				for (int i = 0; i < D; ++i) {
+					if (COPY) {
+						if (row0 + r + i < R)
+							__builtin_nontemporal_store(ring[i],
+										    (g_u32x4w *)(q + (uint64_t)(row0 + r + i) * ROW + 16u * g8));
+					} else {
+						acc ^= ring[i];
+					}
+				}
+			}
+		}
+		if (SYNC)
+			__syncthreads();
+	}
+	if (!COPY && (acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u)
+		out[w] = pad[(threadIdx.x + 1u) & 1023u];
+}
+
+// The other explanation: static shares start on 256 KiB multiples (and their
+// group slices on 32 KiB multiples), so the 32K streams may step through the
+// same HBM channels in phase.  Here each group walks its slice from a hashed
+// starting row (a multiple of D) and wraps around: same shares, same bytes,
+// streams de-phased.
+template <bool COPY, bool ROT>
+__global__ __launch_bounds__(1024, 1) void k_rotated(const uint8_t *p, uint8_t *q, uint32_t R, uint32_t *out)
+{
+	__shared__ uint32_t pad[36 * 1024];
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const PStep s = make_step(r0, r1 - r0, grp);
+	pad[threadIdx.x] = lane;
+	const uint32_t blocks = s.n / D;
+	const uint32_t o = ROT && blocks ? ((((w * 8u + grp) * 2654435761u) >> 9) % blocks) * D : 0u;
+	u32x4 acc = (u32x4)(0u), ring[D];
+	for (uint32_t r = 0; r < s.n; r += D) {
+		uint32_t rows[D];
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			uint32_t j = o + r + i;
+			j = j >= s.n ? j - s.n : j;
+			rows[i] = s.row + min(j, s.n - 1u);
+			ring[i] = ld(p, rows[i], g8);
+		}
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			if (COPY) {
+				if (r + i < s.n)
+					__builtin_nontemporal_store(ring[i], (g_u32x4w *)(q + (uint64_t)rows[i] * ROW + 16u * g8));
+			} else if (r + i < s.n) {
+				acc ^= ring[i];
+			}
+		}
+	}
+	if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u)
+		out[w] = pad[(threadIdx.x + 1u) & 1023u];
+}
+
+// static copy whose stores lag one block: block k+1's loads are issued before
+// block k's stores, so a wait for a load never covers the stores just issued
+// (vmcnt retires loads and stores in issue order).  Two DD-row buffers.
+template <int DD>
+__global__ __launch_bounds__(1024, 1) void k_copy_lag(const uint8_t *p, uint8_t *q, uint32_t R)
+{
+	__shared__ uint32_t pad[36 * 1024];
+	const uint32_t W = gridDim.x * WAVES;
+	const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const PStep s = make_step(r0, r1 - r0, grp);
+	pad[threadIdx.x] = lane;
+	if (s.n == 0)
+		return;
+	u32x4 a[DD], b[DD];
+#pragma unroll
+	for (int i = 0; i < DD; ++i)
+		a[i] = ld(p, s.row + min((uint32_t)i, s.n - 1u), g8);
+	for (uint32_t r = 0; r < s.n; r += 2 * DD) {
+#pragma unroll
+		for (int i = 0; i < DD; ++i)
+			b[i] = ld(p, s.row + min(r + DD + i, s.n - 1u), g8);
+#pragma unroll
+		for (int i = 0; i < DD; ++i)
+			if (r + i < s.n)
+				__builtin_nontemporal_store(a[i], (g_u32x4w *)(q + (uint64_t)(s.row + r + i) * ROW + 16u * g8));
+#pragma unroll
+		for (int i = 0; i < DD; ++i)
+			a[i] = ld(p, s.row + min(r + 2 * DD + i, s.n - 1u), g8);
+#pragma unroll
+		for (int i = 0; i < DD; ++i)
+			if (r + DD + i < s.n)
+				__builtin_nontemporal_store(b[i], (g_u32x4w *)(q + (uint64_t)(s.row + r + DD + i) * ROW + 16u * g8));
+	}
+	if (pad[(threadIdx.x + 1u) & 1023u] == 0x12345678u)
+		q[0] = 0;
+}
+
 // copy variants for the occupancy question: the static copy with DD rows in
 // flight and MINB workgroups per CU (MINB 2: 32 waves per CU, <= 64 VGPRs)
 template <int DD, int MINB>
@@ -1141,6 +1269,50 @@ int main(int argc, char **argv)
 			}
 			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v],
 			       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (all || !strcmp(which, "window")) {
+		const char *names[] = {"read tiles 8 KiB (drifting)", "read tiles 8 KiB, WG lockstep",
+				       "read tiles 32 KiB, WG lockstep", "read grid float4 nt",
+				       "copy tiles 8 KiB (drifting)", "copy tiles 8 KiB, WG lockstep",
+				       "copy tiles 32 KiB, WG lockstep", "copy static, stores lag a block, 2x8 rows",
+				       "copy static, stores lag a block, 2x4 rows", "copy static D8",
+				       "copy grid 1 float4/thread", "read static (pad)", "read static, hashed slice starts",
+				       "copy static (pad)", "copy static, hashed slice starts"};
+		const int nv = (int)(sizeof(names) / sizeof(names[0]));
+		for (int v = 0; v < nv; ++v) {
+			float tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				const uint64_t n16 = bytes / 16;
+				switch (v) {
+				case 0: hipLaunchKernelGGL((k_tiles_sync<false, 64, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 1: hipLaunchKernelGGL((k_tiles_sync<false, 64, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 2: hipLaunchKernelGGL((k_tiles_sync<false, 256, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 3: hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, n16, out); break;
+				case 4: hipLaunchKernelGGL((k_tiles_sync<true, 64, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 5: hipLaunchKernelGGL((k_tiles_sync<true, 64, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 6: hipLaunchKernelGGL((k_tiles_sync<true, 256, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 7: hipLaunchKernelGGL((k_copy_lag<8>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 8: hipLaunchKernelGGL((k_copy_lag<4>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 9: hipLaunchKernelGGL((k_copy_occ<8, 1>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 10: hipLaunchKernelGGL((k_copy_gridk<1>), dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, buf[2], n16); break;
+				case 11: hipLaunchKernelGGL((k_rotated<false, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 12: hipLaunchKernelGGL((k_rotated<false, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 13: hipLaunchKernelGGL((k_rotated<true, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				default: hipLaunchKernelGGL((k_rotated<true, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				}
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			const bool cp = (v >= 4 && v <= 10) || v >= 13;
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"%s\": %.1f}", sep(), names[v], tot / reps * 1e3,
+			       cp ? "GBps_read_plus_write" : "GBps", (cp ? 2.0 : 1.0) * bytes / (tot / reps * 1e-3) / 1e9);
 		}
 	}
 	printf("\n]}\n");
