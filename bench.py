@@ -336,6 +336,7 @@ def main():
         # Python loop not to be the bound
         if len(set(sizes.tolist())) == 1:
             line["msgr_async"] = msgr_c_bench(args, int(sizes[0]), n)
+            line["msgr_cpu"] = msgr_cpu_sizes(args)
         else:
             line["msgr_async"] = msgr_path(args, bufs[0], offs, sizes, outs, P) if n <= 4096 else None
     if rank == 0 and world == 1 and len(shards) == 1 and not args.no_cpu_baseline and not dsts:
@@ -509,7 +510,7 @@ def msgr_path(args, buf0, offs, sizes, outs, P):
             "bytes_per_pass": nbytes, "passes": args.host_passes, "matches_device_path": True}
 
 
-def msgr_c_bench(args, size, count):
+def msgr_c_bench(args, size, count, modes=(("dma", 0), ("zerocopy", 1), ("adapter", 2), ("host", 3))):
     """The messenger-side rate and CPU cost from C (build/msgr_sim bench):
     `count` payloads of `size` bytes in crc32c_pages memory per pass, flushed
     every 64 and completed from an epoll loop, through the async layer (DMA
@@ -523,7 +524,7 @@ def msgr_c_bench(args, size, count):
     exe = os.path.join(REPO, "build", "msgr_sim")
     count = max(1, min(count, (256 << 20) // max(size, 1)))
     res = {}
-    for mode, m in (("dma", 0), ("zerocopy", 1), ("adapter", 2), ("host", 3)):
+    for mode, m in modes:
         r = subprocess.run([exe, "bench", str(size), str(count), str(m), str(args.host_passes)],
                            capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
@@ -531,12 +532,34 @@ def msgr_c_bench(args, size, count):
         d = json.loads(r.stdout.strip().splitlines()[-1])
         res[mode] = {k: d[k] for k in ("GiBps", "payloads_per_s", "thread_cpu_us_per_payload",
                                        "process_cpu_us_per_payload", "latency_us_p50", "latency_us_p99")}
+    if "zerocopy" not in res:
+        return res
     return {"payload_bytes": size, "modes": res, "zerocopy": res["zerocopy"]["GiBps"], "dma": res["dma"]["GiBps"],
             "unit": "GiB/s",
             "path": f"C: {size}-byte payloads in crc32c_pages memory, flush every 64, epoll loop on the eventfd "
                     "(build/msgr_sim bench); dma/zerocopy: crc32c_async_submit per payload; adapter: "
                     "crc32c_msgr_rx_queue/rx_next (host routine up to its cutoff); host: the drop-in crc32c()",
             "payloads": count, "passes": args.host_passes, "matches_oracle": True}
+
+
+def msgr_cpu_sizes(args):
+    """What the messenger's thread pays per payload at the rados.fio sizes
+    (C1/C4: 4 KiB, 64 KiB, 1 MiB, 4 MiB): the adapter (host routine up to its
+    cutoff, the GPU above it) against checksumming on the host with the
+    drop-in, in CPU microseconds per payload of the calling thread and of
+    the process (the HIP runtime's threads included), plus the adapter's
+    submit -> result latency."""
+    out = {}
+    for size in (4096, 65536, 1 << 20, 4 << 20):
+        r = msgr_c_bench(args, size, 16384, modes=(("adapter", 2), ("host", 3)))
+        out[str(size)] = {"adapter_thread_us": r["adapter"]["thread_cpu_us_per_payload"],
+                          "adapter_process_us": r["adapter"]["process_cpu_us_per_payload"],
+                          "host_thread_us": r["host"]["thread_cpu_us_per_payload"],
+                          "adapter_latency_us_p50_p99": [r["adapter"]["latency_us_p50"], r["adapter"]["latency_us_p99"]],
+                          "adapter_GiBps": r["adapter"]["GiBps"], "host_GiBps": r["host"]["GiBps"]}
+    return {"unit": "CPU us per payload", "sizes": out,
+            "path": "build/msgr_sim bench: crc32c_pages payloads, flush every 64, epoll loop; adapter = "
+                    "crc32c_msgr_rx_queue/rx_next, host = drop-in crc32c()"}
 
 
 def sustain(shards, nstreams, seconds, sync_all, dist, backend, dev, torch):

@@ -36,7 +36,10 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <limits.h>
+#include <linux/futex.h>
 #include <stdlib.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <string.h>
 #include <sys/eventfd.h>
@@ -249,6 +252,7 @@ struct Slot {
 	const pech_desc *desc_view = nullptr; // device mapping of h_desc: the plan kernel reads it in place
 	uint32_t *h_out = nullptr, *d_out = nullptr;
 	std::atomic<int> finished{0}; // set by the stream's host function after the results' D2H
+	std::atomic<int> waiting{0};  // a submit sleeps on `finished` (futex): the host function wakes it
 	int efd = -1;                 // the context's eventfd
 	std::vector<Piece> pieces;
 	std::vector<std::pair<size_t, size_t>> packed; // staging runs filled by memcpy: [lo, hi)
@@ -342,11 +346,28 @@ static Slot *slot_new(int efd)
 	return s;
 }
 
+// The slot's `finished` flag doubles as a futex word, so a submit that must
+// wait for a slot sleeps instead of spinning in hipStreamSynchronize: that
+// spin was most of the caller's CPU per payload once the host link is the
+// bound (4 MiB payloads: ~140 us of thread CPU each, profiles/r03/msgr_cpu_v17.txt).
+static_assert(sizeof(std::atomic<int>) == sizeof(int), "futex word");
+static void flag_sleep(std::atomic<int> *f, long ns)
+{
+	struct timespec ts = {0, ns};
+	(void)syscall(SYS_futex, reinterpret_cast<int *>(f), FUTEX_WAIT_PRIVATE, 0, &ts, nullptr, 0);
+}
+
 static void host_notify(void *arg)
 {
-	// HIP runtime thread: only the slot's flag and the eventfd are touched
+	// HIP runtime thread: only the slot's flags and the eventfd are touched.
+	// seq_cst on both sides: either the waiter sees `finished`, or this
+	// thread sees `waiting` and wakes it (a wake before its sleep is not
+	// lost: the futex wait rechecks the word).
 	Slot *s = (Slot *)arg;
-	s->finished.store(1, std::memory_order_release);
+	s->finished.store(1, std::memory_order_seq_cst);
+	if (s->waiting.load(std::memory_order_seq_cst))
+		(void)syscall(SYS_futex, reinterpret_cast<int *>(&s->finished), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr,
+			      nullptr, 0);
 	const uint64_t one = 1;
 	ssize_t r = write(s->efd, &one, sizeof(one));
 	(void)r;
@@ -381,12 +402,22 @@ static int reap(crc32c_async *a, bool wait_oldest, DeviceGuard *dg = nullptr)
 		Slot *s = a->inflight.front();
 		hipError_t q = hipSuccess;
 		if (wait_oldest) {
-			q = hipStreamSynchronize(s->stream);
+			// sleep until the host function marks the slot; a failed stream
+			// never runs it, so the stream is asked every 2 ms
+			s->waiting.store(1, std::memory_order_seq_cst);
+			while (!s->finished.load(std::memory_order_seq_cst)) {
+				flag_sleep(&s->finished, 2000000);
+				if (s->finished.load(std::memory_order_seq_cst))
+					break;
+				q = hipStreamQuery(s->stream);
+				if (q != hipSuccess && q != hipErrorNotReady)
+					break; // failed: its host function will not run
+				(void)hipGetLastError();
+				q = hipSuccess; // (done but not yet marked: the flag comes next)
+			}
+			s->waiting.store(0, std::memory_order_relaxed);
 			if (q == hipSuccess && s->inject_fail)
 				q = hipErrorLaunchFailure; // test build: as a failed stream reports itself
-			while (q == hipSuccess && !s->finished.load(std::memory_order_acquire)) {
-				// the host function runs on the runtime's thread: a moment
-			}
 		} else if (!s->finished.load(std::memory_order_acquire)) {
 			// a failed stream never runs its host function: ask the stream,
 			// once the batch has had kQueryAfterNs to finish (complete() is

@@ -1000,7 +1000,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifdef PECH_NO_POOL // A/B: static shares for every batch
 	const uint32_t jmax = 0u;
 #else
-	const uint32_t jmax = !COPY && uniform ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
+	const uint32_t jmax = !COPY && uniform && wg_rows >= PECH_MAIN_WAVES * PECH_POOL_MIN_SHARE
+				      ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
 										      PECH_MAIN_WAVES) + PECH_ITEM_ROWS - 1u) /
 							     PECH_ITEM_ROWS
 					       : 0u;
