@@ -289,6 +289,7 @@ struct crc32c_async {
 	int efd = -1;
 	bool ready = false; // fully created (destroy drains only then)
 	bool planned_only = false; // PECH_ASYNC_PLANNED=1: every slot on plan + main (A/B measurement)
+	size_t zc_max = kZeroCopyMax; // PECH_ASYNC_ZC_MAX=<bytes>: zero-copy threshold (A/B measurement)
 	std::vector<Slot *> slots;
 	std::deque<Slot *> inflight; // launch order
 	Slot *cur = nullptr;         // slot being filled
@@ -540,6 +541,8 @@ static struct crc32c_async *async_create(unsigned int flags)
 	a->flags = flags;
 	const char *pl = getenv("PECH_ASYNC_PLANNED");
 	a->planned_only = pl && pl[0] == '1';
+	if (const char *zm = getenv("PECH_ASYNC_ZC_MAX"))
+		a->zc_max = (size_t)strtoull(zm, nullptr, 0);
 	if (hipGetDevice(&a->dev) != hipSuccess) {
 		pech_internal_set_err("crc32c_async_create: %s", hipGetErrorString(hipGetLastError()));
 		crc32c_async_destroy(a);
@@ -576,7 +579,7 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 	// one registry lookup: pinned pages are read in place (zero-copy, below
 	// kZeroCopyMax) or DMA'd
 	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
-	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len < kZeroCopyMax ? dv : 0;
+	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len < a->zc_max ? dv : 0;
 	const bool dma = !zc && dv != 0 && len >= kDmaMin;
 	// the common case needs no HIP call: one descriptor into the open slot,
 	// which it does not fill

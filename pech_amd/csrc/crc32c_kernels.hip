@@ -997,6 +997,10 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// to 60 us apart -- end together, and the CU is free for the next
 	// launch's workgroup that much earlier.  (The fused copy keeps static
 	// shares: pooled items cost it 9-14 % per launch, profiles/r02/ab_item_pool.txt.)
+	// Shares below PECH_POOL_MIN_SHARE rows keep static shares too: a 512-row
+	// share (256 MiB of 64 KiB-4 MiB buffers) pooled is a 256-row head and one
+	// item, i.e. runs of 32 rows with a fold each; static, one step of 64-row
+	// runs: 48.8 instead of 51.5-53.4 us per launch (profiles/r03/ab_pool_min_share.txt).
 #ifdef PECH_NO_POOL // A/B: static shares for every batch
 	const uint32_t jmax = 0u;
 #else
@@ -1689,6 +1693,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.17 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches lds-bank-replicated-A128 U" PECH_STR(
-		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS);
+	return "pech_crc32c 0.18 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches lds-bank-replicated-A128 U" PECH_STR(
+		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -47,7 +47,7 @@
 #define PECH_ITEM_ROWS 256u       /* uniform batches: rows per pooled work item */
 #endif
 #ifndef PECH_POOL_MIN_SHARE
-#define PECH_POOL_MIN_SHARE 0u    /* uniform batches pool only shares of at least this many rows */
+#define PECH_POOL_MIN_SHARE 1024u /* uniform batches pool only shares of at least this many rows */
 #endif
 #ifndef PECH_POOL_ROWS
 #define PECH_POOL_ROWS 512u       /* uniform batches: at most this many of a wave's rows are pooled */

@@ -40,6 +40,7 @@ LARGE = C["PECH_LARGE_ROWS"]
 WAVES_PER_WG = C["PECH_MAIN_WAVES"]
 ITEM = C["PECH_ITEM_ROWS"]
 POOL = C.get("PECH_POOL_ROWS", 0xFFFFFFFF)
+POOL_MIN = C.get("PECH_POOL_MIN_SHARE", 0)
 
 
 def share_head(a, b, item=None, pool=None):
@@ -243,7 +244,9 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
     for w0 in range(0, len(ranges), WAVES_PER_WG):
         shares = ranges[w0:w0 + WAVES_PER_WG]
         wg_rows = shares[-1][1] - shares[0][0]
-        jmax = 1 + (min(POOL, (wg_rows + WAVES_PER_WG - 1) // WAVES_PER_WG) + ITEM - 1) // ITEM if uniform else 0
+        # (shares below POOL_MIN rows keep static shares)
+        jmax = (1 + (min(POOL, (wg_rows + WAVES_PER_WG - 1) // WAVES_PER_WG) + ITEM - 1) // ITEM
+                if uniform and wg_rows >= WAVES_PER_WG * POOL_MIN else 0)
         for r0, r1 in shares:
             if r1 > r0:
                 pos, lr = find_start(lrs, pref, nzs, r0)

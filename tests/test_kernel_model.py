@@ -142,3 +142,13 @@ def test_pool_item_and_tail_sizes(monkeypatch, item, pool):
     monkeypatch.setattr(KM, "POOL", pool)
     check([(0x10000 + 4096 * i, 4096) for i in range(1500)], ncu=1)
     check([(0x100000 * (i + 1), 1 << 20) for i in range(3)], ncu=1)
+
+
+@pytest.mark.parametrize("pool_min", [0, 1024])
+def test_pool_min_share(monkeypatch, pool_min):
+    # 512-row shares (the 256 MiB launches of 64 KiB-4 MiB buffers, scaled
+    # down): pooled below the kernel's PECH_POOL_MIN_SHARE only when it is 0,
+    # static shares otherwise; every row consumed once either way
+    monkeypatch.setattr(KM, "POOL_MIN", pool_min)
+    check([(0x100000 * (i + 1), 1 << 16) for i in range(32)], ncu=2)
+    check([(0x100000 * (i + 1), 1 << 20) for i in range(2)], ncu=2)

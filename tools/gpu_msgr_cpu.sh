@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 : > gpurun_out/msgr_cpu.jsonl
 for size in ${SIZES:-4096 16384 65536 262144 1048576 4194304}; do
-  count=$(( (256 << 20) / size )); [ $count -gt 16384 ] && count=16384
+  count=$(( ${BYTES_PER_PASS:-268435456} / size )); [ $count -gt 16384 ] && count=16384
   for mode in ${MODES:-0 1 2 3}; do
     timeout -k 10 120 build/msgr_sim bench $size $count $mode ${PASSES:-3} >> gpurun_out/msgr_cpu.jsonl || { echo "msgr_sim rc=$? size $size mode $mode"; exit 1; }
   done

@@ -651,6 +651,44 @@ __global__ __launch_bounds__(1024, 1) void k_tiles_sync(const uint8_t *p, uint8_
 		out[w] = pad[(threadIdx.x + 1u) & 1023u];
 }
 
+// The grid also deals consecutive 4 KiB pieces to consecutive workgroups, i.e.
+// round robin over the XCDs; k_tiles gives a workgroup 16 consecutive tiles.
+// Here tile t goes to workgroup t mod G first (wave (t / G) mod 16 of it), so
+// neighbouring tiles are on different XCDs, as in the grid.
+template <bool COPY, uint32_t TR>
+__global__ __launch_bounds__(1024, 1) void k_tiles_xcd(const uint8_t *p, uint8_t *q, uint32_t R, uint32_t *out)
+{
+	__shared__ uint32_t pad[36 * 1024];
+	const uint32_t G = gridDim.x, W = G * WAVES;
+	const uint32_t wave = uni(threadIdx.x / 64u);
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	constexpr uint32_t PER = TR / 8u;
+	static_assert(PER % D == 0, "tile slice: whole ring blocks");
+	pad[threadIdx.x] = lane;
+	u32x4 acc = (u32x4)(0u), ring[D];
+	// this wave's tiles: t = k W + wave G + blockIdx.x
+	for (uint32_t t = wave * G + blockIdx.x; (uint64_t)t * TR < R; t += W) {
+		const uint32_t row0 = t * TR + grp * PER;
+		for (uint32_t r = 0; r < PER; r += D) {
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				ring[i] = ld(p, min(row0 + r + i, R - 1u), g8);
+#pragma unroll
+			for (int i = 0; i < D; ++i) {
+				if (COPY) {
+					if (row0 + r + i < R)
+						__builtin_nontemporal_store(ring[i],
+									    (g_u32x4w *)(q + (uint64_t)(row0 + r + i) * ROW + 16u * g8));
+				} else {
+					acc ^= ring[i];
+				}
+			}
+		}
+	}
+	if (!COPY && (acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u)
+		out[blockIdx.x] = pad[(threadIdx.x + 1u) & 1023u];
+}
+
 // The other explanation: static shares start on 256 KiB multiples (and their
 // group slices on 32 KiB multiples), so the 32K streams may step through the
 // same HBM channels in phase.  Here each group walks its slice from a hashed
@@ -1278,7 +1316,9 @@ int main(int argc, char **argv)
 				       "copy tiles 32 KiB, WG lockstep", "copy static, stores lag a block, 2x8 rows",
 				       "copy static, stores lag a block, 2x4 rows", "copy static D8",
 				       "copy grid 1 float4/thread", "read static (pad)", "read static, hashed slice starts",
-				       "copy static (pad)", "copy static, hashed slice starts"};
+				       "copy static (pad)", "copy static, hashed slice starts",
+				       "read tiles 8 KiB, XCD round robin", "copy tiles 8 KiB, XCD round robin",
+				       "copy tiles 32 KiB, XCD round robin"};
 		const int nv = (int)(sizeof(names) / sizeof(names[0]));
 		for (int v = 0; v < nv; ++v) {
 			float tot = 0;
@@ -1301,7 +1341,10 @@ int main(int argc, char **argv)
 				case 11: hipLaunchKernelGGL((k_rotated<false, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
 				case 12: hipLaunchKernelGGL((k_rotated<false, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
 				case 13: hipLaunchKernelGGL((k_rotated<true, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
-				default: hipLaunchKernelGGL((k_rotated<true, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 14: hipLaunchKernelGGL((k_rotated<true, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 15: hipLaunchKernelGGL((k_tiles_xcd<false, 64>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 16: hipLaunchKernelGGL((k_tiles_xcd<true, 64>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				default: hipLaunchKernelGGL((k_tiles_xcd<true, 256>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
 				}
 				CHECK(hipEventRecord(e1, 0));
 				CHECK(hipEventSynchronize(e1));
@@ -1310,7 +1353,7 @@ int main(int argc, char **argv)
 				if (r >= 0)
 					tot += ms;
 			}
-			const bool cp = (v >= 4 && v <= 10) || v >= 13;
+			const bool cp = (v >= 4 && v <= 10) || v == 13 || v == 14 || v >= 16;
 			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"%s\": %.1f}", sep(), names[v], tot / reps * 1e3,
 			       cp ? "GBps_read_plus_write" : "GBps", (cp ? 2.0 : 1.0) * bytes / (tot / reps * 1e-3) / 1e9);
 		}
