@@ -4,6 +4,7 @@ the derived busy fractions (SQ counters are summed over the chip; cycles
 per SQ: GRBM_GUI_ACTIVE / 8 XCDs, per MI355X_MICROARCH.md)."""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 
@@ -12,7 +13,7 @@ def main():
     acc = defaultdict(list)
     for path in sys.argv[1:]:
         for r in csv.DictReader(open(path)):
-            if r["Kernel_Name"] == "pech_crc32c_main":
+            if r["Kernel_Name"] == os.environ.get("PECH_PMC_KERNEL", "pech_crc32c_main"):
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {k: sum(v) / len(v) for k, v in acc.items()}
     out = {"per_dispatch": {k: round(v, 1) for k, v in sorted(avg.items())}}
