@@ -506,7 +506,7 @@ def msgr_path(args, buf0, offs, sizes, outs, P):
         b.free()
     return {"dma": res["dma"], "zerocopy": res["zerocopy"], "unit": "GiB/s",
             "path": "crc32c_async_submit per payload from crc32c_pages memory, flush, drain (eventfd); "
-                    "dma: H2D into 32 MiB device slots; zerocopy: kernel reads pinned pages below 1 MiB in place, larger ones DMA'd",
+                    "dma: H2D into 32 MiB device slots; zerocopy: kernel reads pinned pages in place",
             "bytes_per_pass": nbytes, "passes": args.host_passes, "matches_device_path": True}
 
 

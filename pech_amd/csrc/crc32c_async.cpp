@@ -227,7 +227,11 @@ struct DeviceGuard {
 };
 
 constexpr size_t kSlotBytes = 32u << 20; // staging per slot
-constexpr size_t kZeroCopyMax = 1u << 20; // pinned payloads from this size up are DMA'd even in zero-copy mode
+// CRC32C_ASYNC_ZEROCOPY reads every pinned payload in place.  Until round 3
+// payloads from 1 MiB up were DMA'd even then: a little more link bandwidth
+// (42-50 against 36-37 GiB/s), but 5-40 us of the caller's CPU per payload
+// against 0.6 (profiles/r03/ab_zc_max.txt); pech's one thread is the budget.
+constexpr size_t kZeroCopyMax = SIZE_MAX;
 // DMA mode: pinned payloads below this are packed into the slot's staging by
 // memcpy (one H2D per slot) instead of one hipMemcpyAsync each: a DMA call
 // costs the caller microseconds of CPU, a 4 KiB memcpy a fraction of one
@@ -256,7 +260,8 @@ struct Slot {
 	int efd = -1;                 // the context's eventfd
 	std::vector<Piece> pieces;
 	std::vector<std::pair<size_t, size_t>> packed; // staging runs filled by memcpy: [lo, hi)
-	size_t used = 0;
+	size_t used = 0;     // staging bytes
+	size_t zc_bytes = 0; // bytes read in place: a slot launches at kSlotBytes of either
 	uint32_t maxlen = 0; // longest piece: the direct kernel takes slots of pieces below kDirectMax
 	bool inflight = false;
 	bool inject_fail = false; // test build: this batch's stream "failed" (PECH_FAULT_ASYNC_STREAM)
@@ -391,6 +396,7 @@ static void harvest(crc32c_async *a, Slot *s, int err)
 	s->pieces.clear();
 	s->packed.clear();
 	s->used = 0;
+	s->zc_bytes = 0;
 	s->maxlen = 0;
 	s->inflight = false;
 	s->inject_fail = false;
@@ -584,7 +590,7 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 	// the common case needs no HIP call: one descriptor into the open slot,
 	// which it does not fill
 	const Slot *c = a->cur;
-	const bool quiet = c && !dma && c->pieces.size() + 1u < kSlotDescs && (zc || c->used + len + 512u < kSlotBytes);
+	const bool quiet = c && !dma && c->pieces.size() + 1u < kSlotDescs && (zc ? c->zc_bytes + len < kSlotBytes : c->used + len + 512u < kSlotBytes);
 	DeviceGuard dg(a->dev, !quiet);
 	if (!quiet && !dg.ok) {
 		pech_internal_set_err("crc32c_async_submit: cannot select device %d", a->dev);
@@ -619,6 +625,7 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 		if (zc) {
 			piece = left; // read in place: no staging space
 			d.addr = zc + (len - left);
+			s->zc_bytes += piece;
 		} else {
 			piece = left < kSlotBytes - s->used ? left : kSlotBytes - s->used;
 			d.addr = (uint64_t)(uintptr_t)(s->d_stage + s->used);
@@ -653,7 +660,7 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 	it.placed = true;
 	it.total = placed;
 	Slot *s = a->cur;
-	if (s && (s->pieces.size() == kSlotDescs || s->used >= kSlotBytes)) {
+	if (s && (s->pieces.size() == kSlotDescs || s->used >= kSlotBytes || s->zc_bytes >= kSlotBytes)) {
 		const int rc = launch_slot(a);
 		// This payload filled the slot and its launch failed: its pieces are
 		// harvested with the error, but the submission returns it, so the
