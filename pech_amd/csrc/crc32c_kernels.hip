@@ -1533,6 +1533,21 @@ __device__ __forceinline__ void finish_direct(uint32_t *lds, uint32_t g8, uint32
 		out[STEP_ORIG(S)] = v;
 }
 
+// Direct mode: a ring load past the run's last row (the unrolled tail of its
+// last block, the final prefetch) only keeps the ring's counted order, so it
+// reads the constants table (L2-resident) instead of the run's last line
+// again.  (The bounds-checked build keeps the in-buffer clamp it can check.)
+__device__ __forceinline__ uint64_t dload_addr(const Step &S, uint32_t row, uint32_t last, uint64_t dummy)
+{
+#if defined(PECH_DEBUG_BOUNDS) || defined(PECH_DIRECT_CLAMP) // (PECH_DIRECT_CLAMP: A/B, the v0.18 clamp)
+	(void)dummy;
+	return row_addr(S.ad, min(row, last), STEP_ZOFF(S));
+#else
+	const uint64_t a = row_addr(S.ad, min(row, last), STEP_ZOFF(S));
+	return row <= last ? a : dummy;
+#endif
+}
+
 template <uint32_t U>
 __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__restrict__ descs, uint32_t n,
 					    const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
@@ -1559,6 +1574,9 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
 	uint32_t pos = (uint32_t)((uint64_t)wglob * n / W), ph = 0;
 	const uint32_t pend = (uint32_t)((uint64_t)(wglob + 1u) * n / W);
+	// (spread over 128 lines of the table: one line for every wave was an L2 hot spot)
+	const uint64_t dummy = (uint64_t)consts + (uint64_t)((wglob * 8u + grp) & 127u) * PECH_ROW_BYTES + 16u * g8;
+	static_assert(128u * PECH_ROW_BYTES <= PECH_C_WORDS * 4u, "dummy lines inside the constants");
 	Step S = plan_direct(descs, consts, pos, pend, ph, g8, grp);
 	u32x4 ring[U];
 	if (S.T)
@@ -1603,24 +1621,24 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 			const uint32_t r = blk * U;
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
-				ring[(i + U - 1) % U] = LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
+				ring[(i + U - 1) % U] = LD_PIECE(S, dload_addr(S, r + i + U - 1, last, dummy), 3);
 				horner_row_pred(lds, lreg, tail_keep(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 			}
 		}
 		const uint32_t r = blk * U;
-		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
+		ring[U - 1] = LD_PIECE(S, dload_addr(S, r + U - 1, last, dummy), 4);
 		const Step N = plan_direct(descs, consts, pos, pend, ph, g8, grp);
 		// the last block's rows past every group's run (S.T, wave-uniform)
 		// are skipped by a scalar branch: their loads keep the ring's order
 		if (r < S.T)
 			horner_row_pred(lds, lreg, tail_keep(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
-		// branch-free: with no next step the prefetch re-reads this step's last row
+		// branch-free: with no next step the prefetch reads the constants
 		const bool more = N.T != 0;
 		const Step &L = more ? N : S;
-		const uint32_t lrow0 = more ? 0u : last, lmax = more ? N.nl - 1u : last;
+		const uint32_t lmax = more ? N.nl - 1u : last;
 #pragma unroll
 		for (uint32_t i = 1; i < U; ++i) {
-			ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
+			ring[i - 1] = LD_PIECE(L, dload_addr(L, more ? i - 1 : lmax + 1u, lmax, dummy), 5);
 			if (r + i < S.T)
 				horner_row_pred(lds, lreg, tail_keep(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 		}
@@ -1693,6 +1711,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.18 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.19 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }
