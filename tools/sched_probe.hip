@@ -730,6 +730,63 @@ __global__ __launch_bounds__(1024, 1) void k_rotated(const uint8_t *p, uint8_t *
 		out[w] = pad[(threadIdx.x + 1u) & 1023u];
 }
 
+// Split roles: waves 0-7 of a workgroup only load (their vmcnt never holds a
+// store), stage each 8-row block in LDS and hand it to their partner wave
+// 8-15, which only stores (and so never waits for anything but its LDS
+// slot).  Two 8 KiB slots per pair, LDS flags polled with s_sleep.  Tests
+// whether the persistent copy's deficit against the grid is a wave waiting
+// on its own store acknowledgements.
+__global__ __launch_bounds__(1024, 1) void k_copy_split(const uint8_t *p, uint8_t *q, uint32_t R)
+{
+	__shared__ __attribute__((aligned(16))) u32x4 stage[8][2][D * 64]; // 128 KiB
+	__shared__ uint32_t flag[8][2];
+	const uint32_t wave = uni(threadIdx.x / 64u), pair = wave & 7u;
+	const bool reader = wave < 8u;
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t W = gridDim.x * 8u, w = blockIdx.x * 8u + pair; // shares per pair
+	const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+	const PStep s = make_step(r0, r1 - r0, grp);
+	if (threadIdx.x < 16u)
+		flag[threadIdx.x >> 1][threadIdx.x & 1u] = 0u;
+	__syncthreads();
+	const uint32_t nb = (s.T + D - 1u) / D; // blocks (wave-uniform: T)
+	for (uint32_t b = 0; b < nb; ++b) {
+		const uint32_t k = b & 1u, r = b * D;
+		volatile uint32_t *f = &flag[pair][k];
+		if (reader) {
+			u32x4 v[D];
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				v[i] = ld(p, s.row + min(r + i, s.n - 1u), g8);
+			while (*f != 0u)
+				__builtin_amdgcn_s_sleep(1);
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				stage[pair][k][i * 64 + lane] = v[i];
+			__builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the slot's writes are done
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+			if (lane == 0)
+				*f = 1u;
+		} else {
+			while (*f != 1u)
+				__builtin_amdgcn_s_sleep(1);
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+			u32x4 v[D];
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				v[i] = stage[pair][k][i * 64 + lane];
+			__builtin_amdgcn_s_waitcnt(0xc07f);
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+			if (lane == 0)
+				*f = 0u;
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				if (r + i < s.n)
+					__builtin_nontemporal_store(v[i], (g_u32x4w *)(q + (uint64_t)(s.row + r + i) * ROW + 16u * g8));
+		}
+	}
+}
+
 // static copy whose stores lag one block: block k+1's loads are issued before
 // block k's stores, so a wait for a load never covers the stores just issued
 // (vmcnt retires loads and stores in issue order).  Two DD-row buffers.
@@ -1307,6 +1364,44 @@ int main(int argc, char **argv)
 			}
 			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v],
 			       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (!strcmp(which, "copysplit")) {
+		const char *names[] = {"copy static D8", "copy split roles (8 loading + 8 storing waves, LDS hand-off)",
+				       "copy grid 1 float4/thread"};
+		for (int v = 0; v < 3; ++v) {
+			float tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				const uint64_t n16 = bytes / 16;
+				switch (v) {
+				case 0: hipLaunchKernelGGL((k_copy_occ<8, 1>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 1: hipLaunchKernelGGL(k_copy_split, dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				default: hipLaunchKernelGGL((k_copy_gridk<1>), dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, buf[2], n16); break;
+				}
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v],
+			       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+		// the split copy's destination must equal its source
+		std::vector<uint8_t> h0(1 << 20), h1(1 << 20);
+		hipLaunchKernelGGL(k_copy_split, dim3(ncu), dim3(1024), 0, 0, buf[0], buf[2], R);
+		CHECK(hipDeviceSynchronize());
+		for (size_t off = 0; off < bytes; off += bytes / 7) {
+			const size_t o = off & ~(size_t)((1 << 20) - 1);
+			CHECK(hipMemcpy(h0.data(), buf[0] + o, 1 << 20, hipMemcpyDeviceToHost));
+			CHECK(hipMemcpy(h1.data(), buf[2] + o, 1 << 20, hipMemcpyDeviceToHost));
+			if (memcmp(h0.data(), h1.data(), 1 << 20)) {
+				printf("\n  {\"error\": \"split copy differs at %zu\"}", o);
+				break;
+			}
 		}
 	}
 	if (all || !strcmp(which, "window")) {
