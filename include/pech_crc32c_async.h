@@ -76,7 +76,7 @@ typedef void (*crc32c_done_fn)(void *arg, uint32_t crc, int err);
  * pays well under a microsecond per payload at any size.  Without the flag,
  * pinned payloads from 32 KiB up are DMA'd to device slots: more link
  * bandwidth for large payloads (MI355X: 42-50 vs 36-37 GiB/s at 1-4 MiB)
- * at 5-27 us of the caller's CPU per payload. */
+ * at 5-85 us of the caller's CPU per payload. */
 #define CRC32C_ASYNC_ZEROCOPY 1u
 
 /* A context on the current device: its own HIP stream, staging slots and

@@ -691,6 +691,8 @@ extern "C" int crc32c_async_flush(struct crc32c_async *a)
 		return -EINVAL;
 	if (a->err)
 		return a->err;
+	if (!a->cur || a->cur->pieces.empty())
+		return 0; // nothing to launch: no device guard, no stack switch
 	return on_lib_stack([&] {
 		DeviceGuard dg(a->dev);
 		return launch_slot(a);

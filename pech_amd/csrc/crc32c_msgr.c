@@ -67,7 +67,11 @@ struct crc32c_msgr_conn {
 	crc32c_msgr_kick_fn kick;
 	void *kick_arg;
 	crc32c_msgr_release_fn release;
+	struct rx_ent *rx_cache; /* retired receive entries for reuse (host-routed payloads churn them) */
+	unsigned int nrx_cache;
 };
+
+#define RX_CACHE_MAX 256u
 
 static struct crc32c_msgr_stats g_st;
 static unsigned int g_host_max = PECH_MSGR_HOST_MAX_DEFAULT;
@@ -142,6 +146,30 @@ struct crc32c_msgr_conn *crc32c_msgr_conn_create(struct crc32c_async *a, unsigne
 	return c;
 }
 
+static struct rx_ent *rx_alloc(struct crc32c_msgr_conn *c)
+{
+	struct rx_ent *e = c->rx_cache;
+
+	if (!e)
+		return calloc(1, sizeof(*e));
+	c->rx_cache = e->next;
+	c->nrx_cache--;
+	memset(e, 0, sizeof(*e));
+	return e;
+}
+
+/* a retired entry of connection c (never an orphan: those are freed where they land) */
+static void rx_retire(struct crc32c_msgr_conn *c, struct rx_ent *e)
+{
+	if (c->nrx_cache >= RX_CACHE_MAX) {
+		free(e);
+		return;
+	}
+	e->next = c->rx_cache;
+	c->rx_cache = e;
+	c->nrx_cache++;
+}
+
 int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data, unsigned int len, int check,
 			 uint32_t footer_crc)
 {
@@ -151,7 +179,7 @@ int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data
 		return -EINVAL;
 	if (c->npending >= c->max_pending && msg) /* skip markers hold no message: always taken */
 		return -EAGAIN;
-	e = calloc(1, sizeof(*e));
+	e = rx_alloc(c);
 	if (!e)
 		return -ENOMEM;
 	e->conn = c;
@@ -211,7 +239,7 @@ int crc32c_msgr_rx_next(struct crc32c_msgr_conn *c, void **msg, uint32_t *crc)
 	} else if (e->check) {
 		g_st.rx_verified++;
 	}
-	free(e);
+	rx_retire(c, e);
 	return rc;
 }
 
@@ -418,7 +446,7 @@ void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c)
 			if (e->msg) /* NULL: an in-order skip marker */
 				c->release(e->msg);
 			g_st.rx_released++;
-			free(e);
+			rx_retire(c, e);
 		}
 	}
 	c->head = c->tail = NULL;
@@ -431,6 +459,12 @@ void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c)
 		return;
 	crc32c_msgr_conn_reset(c);
 	crc32c_msgr_tx_cancel(c, NULL);
+	while (c->rx_cache) {
+		struct rx_ent *e = c->rx_cache;
+
+		c->rx_cache = e->next;
+		free(e);
+	}
 	free(c);
 }
 
