@@ -787,6 +787,61 @@ __global__ __launch_bounds__(1024, 1) void k_copy_split(const uint8_t *p, uint8_
 	}
 }
 
+// Workgroup-interleaved rows: workgroup b owns a contiguous share of the
+// batch, and its 128 lane groups walk it together -- group j of the
+// workgroup takes rows j, j + 128, j + 256, ... of the share, so one row
+// step of the workgroup reads (and writes) 16 KiB contiguous, and the CU's
+// footprint in flight is one contiguous window.  (A CRC run over rows 128
+// apart is Horner with x^(8 * 16 KiB) instead of x^(8 * 128): the same table
+// size.)  D rows in flight per lane.
+template <bool COPY>
+__global__ __launch_bounds__(1024, 1) void k_wg_interleave(const uint8_t *p, uint8_t *q, uint32_t R, uint32_t *out)
+{
+	__shared__ uint32_t pad[36 * 1024];
+	const uint32_t G = gridDim.x, b = blockIdx.x;
+	const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u;
+	const uint32_t j = threadIdx.x >> 3; // lane group of the workgroup, 0..127
+	const uint32_t r0 = (uint32_t)((uint64_t)R * b / G), r1 = (uint32_t)((uint64_t)R * (b + 1u) / G);
+	pad[threadIdx.x] = lane;
+	const uint32_t n = r1 - r0, steps = (n + 127u) / 128u; // row steps of the workgroup
+	u32x4 acc = (u32x4)(0u), ring[D];
+	for (uint32_t k = 0; k < steps; k += D) {
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			const uint32_t rr = (k + i) * 128u + j;
+			ring[i] = ld(p, r0 + min(rr, n - 1u), g8);
+		}
+#pragma unroll
+		for (int i = 0; i < D; ++i) {
+			const uint32_t rr = (k + i) * 128u + j;
+			if (rr < n) {
+				if (COPY)
+					__builtin_nontemporal_store(ring[i], (g_u32x4w *)(q + (uint64_t)(r0 + rr) * ROW + 16u * g8));
+				else
+					acc ^= ring[i];
+			}
+		}
+	}
+	if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u)
+		out[b] = pad[(threadIdx.x + 1u) & 1023u];
+}
+
+// grid copy with one float4 per thread, workgroups of NT threads holding
+// PADW words of LDS (occupancy control)
+template <int NT, int PADW>
+__global__ __launch_bounds__(NT) void k_copy_grid_pad(const uint8_t *p, uint8_t *q, uint64_t n16)
+{
+	__shared__ uint32_t pad[PADW];
+	const uint64_t i = blockIdx.x * (uint64_t)NT + threadIdx.x;
+	pad[threadIdx.x % PADW] = threadIdx.x;
+	if (i < n16) {
+		u32x4 v = __builtin_nontemporal_load((g_u32x4 *)(p + 16u * i));
+		if (pad[(threadIdx.x + 1) % PADW] == 0x12345678u)
+			v.x = 0;
+		__builtin_nontemporal_store(v, (g_u32x4w *)(q + 16u * i));
+	}
+}
+
 // static copy whose stores lag one block: block k+1's loads are issued before
 // block k's stores, so a wait for a load never covers the stores just issued
 // (vmcnt retires loads and stores in issue order).  Two DD-row buffers.
@@ -1364,6 +1419,42 @@ int main(int argc, char **argv)
 			}
 			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v],
 			       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (!strcmp(which, "copyshape")) {
+		const char *names[] = {"copy static D8", "copy grid 1 float4/thread (256-thread WGs)",
+				       "copy grid 1 float4/thread, 1024-thread WGs", "copy grid 1 float4/thread, 256 threads + 40 KiB LDS (4 WGs/CU)",
+				       "copy grid 1 float4/thread, 1024 threads + 144 KiB LDS (1 WG/CU)",
+				       "copy workgroup-interleaved rows (128 groups, 16 KiB per row step)",
+				       "read workgroup-interleaved rows", "read static (pad)", "read grid float4 nt"};
+		const int nv = (int)(sizeof(names) / sizeof(names[0]));
+		for (int v = 0; v < nv; ++v) {
+			float tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				const uint64_t n16 = bytes / 16;
+				switch (v) {
+				case 0: hipLaunchKernelGGL((k_copy_occ<8, 1>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R); break;
+				case 1: hipLaunchKernelGGL((k_copy_gridk<1>), dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, buf[2], n16); break;
+				case 2: hipLaunchKernelGGL((k_copy_grid_pad<1024, 64>), dim3((unsigned)(n16 / 1024)), dim3(1024), 0, 0, src, buf[2], n16); break;
+				case 3: hipLaunchKernelGGL((k_copy_grid_pad<256, 10 * 1024>), dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, buf[2], n16); break;
+				case 4: hipLaunchKernelGGL((k_copy_grid_pad<1024, 36 * 1024>), dim3((unsigned)(n16 / 1024)), dim3(1024), 0, 0, src, buf[2], n16); break;
+				case 5: hipLaunchKernelGGL((k_wg_interleave<true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 6: hipLaunchKernelGGL((k_wg_interleave<false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 7: hipLaunchKernelGGL((k_rotated<false, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				default: hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, n16, out); break;
+				}
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			const bool cp = v <= 5;
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"%s\": %.1f}", sep(), names[v], tot / reps * 1e3,
+			       cp ? "GBps_read_plus_write" : "GBps", (cp ? 2.0 : 1.0) * bytes / (tot / reps * 1e-3) / 1e9);
 		}
 	}
 	if (!strcmp(which, "copysplit")) {
