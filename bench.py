@@ -336,7 +336,10 @@ def main():
         # Python loop not to be the bound
         if len(set(sizes.tolist())) == 1:
             line["msgr_async"] = msgr_c_bench(args, int(sizes[0]), n)
-            line["msgr_cpu"] = msgr_cpu_sizes(args)
+            try:  # an auxiliary leg: its failure is reported in the line, not fatal to it
+                line["msgr_cpu"] = msgr_cpu_sizes(args)
+            except (SystemExit, Exception) as e:  # noqa: BLE001
+                line["msgr_cpu"] = {"error": str(e)[:500]}
         else:
             line["msgr_async"] = msgr_path(args, bufs[0], offs, sizes, outs, P) if n <= 4096 else None
     if rank == 0 and world == 1 and len(shards) == 1 and not args.no_cpu_baseline and not dsts:
