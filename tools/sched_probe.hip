@@ -794,7 +794,7 @@ __global__ __launch_bounds__(1024, 1) void k_copy_split(const uint8_t *p, uint8_
 // footprint in flight is one contiguous window.  (A CRC run over rows 128
 // apart is Horner with x^(8 * 16 KiB) instead of x^(8 * 128): the same table
 // size.)  D rows in flight per lane.
-template <bool COPY>
+template <bool COPY, bool SYNC = false>
 __global__ __launch_bounds__(1024, 1) void k_wg_interleave(const uint8_t *p, uint8_t *q, uint32_t R, uint32_t *out)
 {
 	__shared__ uint32_t pad[36 * 1024];
@@ -821,6 +821,8 @@ __global__ __launch_bounds__(1024, 1) void k_wg_interleave(const uint8_t *p, uin
 					acc ^= ring[i];
 			}
 		}
+		if (SYNC)
+			__syncthreads(); // the workgroup's 16 waves stay on one window
 	}
 	if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u)
 		out[b] = pad[(threadIdx.x + 1u) & 1023u];
@@ -1426,7 +1428,10 @@ int main(int argc, char **argv)
 				       "copy grid 1 float4/thread, 1024-thread WGs", "copy grid 1 float4/thread, 256 threads + 40 KiB LDS (4 WGs/CU)",
 				       "copy grid 1 float4/thread, 1024 threads + 144 KiB LDS (1 WG/CU)",
 				       "copy workgroup-interleaved rows (128 groups, 16 KiB per row step)",
-				       "read workgroup-interleaved rows", "read static (pad)", "read grid float4 nt"};
+				       "read workgroup-interleaved rows", "read static (pad)", "read grid float4 nt",
+				       "read workgroup-interleaved rows, barrier per 8-row block",
+				       "copy workgroup-interleaved rows, barrier per 8-row block",
+				       "read tiles 8 KiB, WG lockstep"};
 		const int nv = (int)(sizeof(names) / sizeof(names[0]));
 		for (int v = 0; v < nv; ++v) {
 			float tot = 0;
@@ -1443,7 +1448,10 @@ int main(int argc, char **argv)
 				case 5: hipLaunchKernelGGL((k_wg_interleave<true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
 				case 6: hipLaunchKernelGGL((k_wg_interleave<false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
 				case 7: hipLaunchKernelGGL((k_rotated<false, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
-				default: hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, n16, out); break;
+				case 8: hipLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(n16 / 256)), dim3(256), 0, 0, src, n16, out); break;
+				case 9: hipLaunchKernelGGL((k_wg_interleave<false, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 10: hipLaunchKernelGGL((k_wg_interleave<true, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				default: hipLaunchKernelGGL((k_tiles_sync<false, 64, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
 				}
 				CHECK(hipEventRecord(e1, 0));
 				CHECK(hipEventSynchronize(e1));
@@ -1452,7 +1460,7 @@ int main(int argc, char **argv)
 				if (r >= 0)
 					tot += ms;
 			}
-			const bool cp = v <= 5;
+			const bool cp = v <= 5 || v == 10;
 			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"%s\": %.1f}", sep(), names[v], tot / reps * 1e3,
 			       cp ? "GBps_read_plus_write" : "GBps", (cp ? 2.0 : 1.0) * bytes / (tot / reps * 1e-3) / 1e9);
 		}
