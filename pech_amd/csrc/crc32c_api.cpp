@@ -87,6 +87,13 @@ static void build_consts(uint32_t *c)
 	// A_1: the reference byte table (include/crc32c.h:16-81), regenerated
 	for (uint32_t e = 0; e < 256; ++e)
 		c[PECH_C_TAB1 + e] = gf2_mulmod(CRC32C_X8, e);
+	// A_16384: the fused copy's Horner step over rows 128 apart (interleaved mode)
+	{
+		const uint32_t xk = gf2_x8n((uint64_t)PECH_IL_GROUPS * PECH_ROW_BYTES);
+		for (uint32_t k = 0; k < 4; ++k)
+			for (uint32_t e = 0; e < 256; ++e)
+				c[PECH_C_TAB16K + k * 256u + e] = gf2_mulmod(xk, e << (8 * k));
+	}
 	// XINV[k] = x^(-8k): undoes k trailing zero bytes (a core's last line)
 	const uint32_t xinv8 = gf2_xinv8n(1);
 	uint32_t acc = CRC32C_ONE;

@@ -494,9 +494,9 @@ struct Step {
 // zeroed after its load, and without the barrier LLVM treats the load's
 // address as "don't care" in that case and folds ad + zoff back to ad -- a
 // read before the buffer (seen in the ISA; a GPU fault at allocation starts).
-__device__ __forceinline__ uint64_t row_addr(uint64_t ad, uint32_t row, uint32_t zoff)
+__device__ __forceinline__ uint64_t row_addr(uint64_t ad, uint32_t row, uint32_t zoff, uint32_t rs = PECH_ROW_BYTES)
 {
-	uint64_t a = ad + (uint64_t)row * PECH_ROW_BYTES + (row == 0 ? zoff : 0u);
+	uint64_t a = ad + (uint64_t)row * rs + (row == 0 ? zoff : 0u);
 	asm("" : "+v"(a));
 	return a;
 }
@@ -741,6 +741,86 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 	return S;
 }
 
+// Fused copy, interleaved rows (uniform batches of buffers of at least
+// PECH_IL_MIN_ROWS rows): the workgroup's 128 lane groups walk the portion
+// [lr, lr + P) of one buffer together, group j taking rows lr + j,
+// lr + j + 128, ... (`ad` steps 16 KiB per row; Horner over rows 128 apart
+// is A_16384, the LDS table in this mode).  One row step of the workgroup
+// reads and writes 16 KiB contiguous, so the CU's accesses in flight form
+// one window instead of 128 scattered slices (copy probe: 389.5 against
+// 407.0 us per GiB, profiles/r03/copyshape_probe.json).  The cursor is the
+// workgroup's, the same in all its waves.
+template <bool COPY>
+__device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
+					uint32_t pos, uint32_t lr, uint32_t rem, uint32_t j, uint32_t g8)
+{
+	Step S;
+	int64_t dl = 0;
+	S.T = 0;
+	S.nmin = 0;
+	S.ad = 0;
+	S.mp = 0;
+	S.nl = 1;
+	S.nu = 0;
+	S.oz = 0;
+#ifdef PECH_DEBUG_BOUNDS
+	S.blo = S.bhi = 0;
+#endif
+	if (rem) {
+		const pech_core cd = cores[pos]; // wave-uniform: scalar loads
+		const uint32_t rows0 = uni(cd.rows);
+		const uint64_t a0 = uni64(cd.addr);
+		const uint64_t vb0 = a0 & ~(uint64_t)(PECH_ROW_BYTES - 1u);
+		const uint32_t lb0 = (uint32_t)a0 & (PECH_ROW_BYTES - 1u);
+		const uint32_t meta0 = uni(cd.meta);
+		const uint32_t zt0 = PECH_META_ZT(meta0);
+		const uint32_t P = min(rows0 - lr, rem);
+		const uint32_t nn = P > j ? (P - j + PECH_IL_GROUPS - 1u) / PECH_IL_GROUPS : 0u;
+		const uint32_t st = lr + j;
+		// the wave's 8 groups are j0..j0+7: counts nonincreasing in the group
+		const uint32_t j0 = j & ~7u;
+		S.T = P > j0 ? (P - j0 + PECH_IL_GROUPS - 1u) / PECH_IL_GROUPS : 0u;
+		uint32_t tmin = S.T;
+#pragma unroll
+		for (uint32_t g = 1; g < 8; ++g) {
+			const uint32_t c = P > j0 + g ? (P - j0 - g + PECH_IL_GROUPS - 1u) / PECH_IL_GROUPS : 0u;
+			tmin = c ? c : tmin;
+		}
+		S.nmin = tmin;
+		if (nn) {
+			const uint32_t last = st + PECH_IL_GROUPS * (nn - 1u);
+			S.ad = vb0 + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
+			S.nl = nn;
+			S.nu = nn;
+			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) | tail_bits(last == rows0 - 1u, g8, zt0);
+			S.mp = ((rows0 - last - 1u) << 7) | (meta0 >> 16 & 0x70u) | PECH_META_TAIL(meta0);
+		} else {
+			// an idle group reloads the portion's first row (valid memory,
+			// the redirect of row 0's pieces before the buffer kept), ignored
+			S.ad = vb0 + (uint64_t)lr * PECH_ROW_BYTES + 16u * g8;
+			S.oz = head_bits(lr == 0, g8, lb0) & (7u << 20);
+		}
+		if (COPY)
+			dl = deltas[PECH_META_ORIG(meta0)];
+#ifdef PECH_DEBUG_BOUNDS
+		S.blo = vb0 + 16u * (lb0 >> 4);
+		S.bhi = vb0 + (uint64_t)rows0 * PECH_ROW_BYTES;
+#endif
+		rem -= P;
+		if (lr + P == rows0) {
+			++pos;
+			lr = 0;
+		} else {
+			lr += P;
+		}
+	}
+	S.pos = pos;
+	S.lr = lr;
+	S.rem = rem;
+	S.dad = S.ad + (uint64_t)dl;
+	return S;
+}
+
 #define STEP_ZOFF(S) (((S).oz >> 16) & 0x70u) // (zoff/16) << 20 -> zoff
 #define STEP_ORIG(S) ((S).oz & 0xFFFFFu)
 #define STEP_ZH(S) (((S).oz >> 23) & 15u)
@@ -754,12 +834,13 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 // slot ever holds two live values: the register mapping is static across
 // the loop back-edge (no copies, and no vmcnt(0) drain to make them).
 // Priming loads rows 0..PECH_U-2 (clamped to the step's rows).
-#define RING_PRIME(S, ring)                                                                           \
+#define RING_PRIME_RS(S, ring, rs)                                                                     \
 	do {                                                                                          \
 		const uint32_t last_ = (S).nl - 1u;                                                   \
 		_Pragma("unroll") for (uint32_t i = 0; i + 1 < U; ++i) (ring)[i] =                    \
-			LD_PIECE((S), row_addr((S).ad, min(i, last_), STEP_ZOFF(S)), 1);                 \
+			LD_PIECE((S), row_addr((S).ad, min(i, last_), STEP_ZOFF(S), (rs)), 1);           \
 	} while (0)
+#define RING_PRIME(S, ring) RING_PRIME_RS(S, ring, PECH_ROW_BYTES)
 
 __device__ __forceinline__ void horner_row(const uint32_t *lds, uint32_t lreg, u32x4 w, uint32_t &s0, uint32_t &s1,
 					   uint32_t &s2, uint32_t &s3)
@@ -848,11 +929,11 @@ __device__ __forceinline__ bool zl_keep(const Step &S, uint32_t row)
 // one --, trailing virtual pieces) and rows past nu (clamped prefetch, idle
 // groups) are never stored.
 template <bool COPY>
-__device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, bool ok)
+__device__ __forceinline__ void st_piece(const Step &S, uint32_t row, u32x4 v, bool ok, uint32_t rs = PECH_ROW_BYTES)
 {
 	typedef __attribute__((address_space(1))) u32x4 g_u32x4w;
 	if (COPY && ok) // nontemporal: the destination is not re-read by this launch
-		__builtin_nontemporal_store(v, (g_u32x4w *)(S.dad + (uint64_t)row * PECH_ROW_BYTES));
+		__builtin_nontemporal_store(v, (g_u32x4w *)(S.dad + (uint64_t)row * rs));
 }
 
 // Uniform batches: the end of share [a, b)'s head, which its owner walks
@@ -897,10 +978,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	constexpr uint32_t NT4 = (PECH_C_TAB1 - PECH_C_TAB4) / 4u; // single-copy tables, 16-B words
 	constexpr uint32_t TPT = (NT4 + PECH_MAIN_THREADS - 1u) / PECH_MAIN_THREADS;
 	const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
-	uint32_t t128[T128];
+	uint32_t t128[T128], t16k[T128];
 #pragma unroll
-	for (uint32_t j = 0; j < T128; ++j)
+	for (uint32_t j = 0; j < T128; ++j) {
 		t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
+		t16k[j] = COPY ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS] : 0u; // interleaved mode's table
+	}
 	u32x4 tv[TPT];
 #pragma unroll
 	for (uint32_t k = 0; k < TPT; ++k)
@@ -968,6 +1051,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	for (uint32_t k = 0; k < 16; ++k)
 		uok = uok && (uint64_t)(nc[k] & PECH_NZ_MASK) * U0 == (uint64_t)pc[k];
 	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
+	// fused copy of a uniform batch of large buffers: interleaved rows (plan_il)
+	const bool il = PECH_IL_COPY && COPY && uniform && U0 >= PECH_IL_MIN_ROWS;
+	const uint32_t rsb = il ? PECH_IL_GROUPS * PECH_ROW_BYTES : PECH_ROW_BYTES; // bytes from one row of a run to the next
 	STAMP(t_scan);
 	// Every wave gets an equal share of the batch's rows (at least rpw_min).
 	// Large batches: workgroup b gets rows [b Rtot / G, (b+1) Rtot / G) --
@@ -1126,10 +1212,16 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		}
 	}
 	STAMP(t_find);
-	Step S = plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
+	if (il) { // the workgroup's whole range, walked by all its waves together
+		p0 = (uint32_t)(wg0 / U0);
+		lr0 = (uint32_t)(wg0 - (uint64_t)p0 * U0);
+		rem_all = wg_rows;
+	}
+	Step S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
+		    : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
 	STAMP(t_plan);
 	if (S.T)
-		RING_PRIME(S, ring);
+		RING_PRIME_RS(S, ring, rsb);
 
 	// The LDS tables, needed from the first row on, written while the prime
 	// is in flight.  A_128 once per bank: its 32 copies as 8 x 16 B; lane t
@@ -1139,7 +1231,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 	for (uint32_t j = 0; j < T128; ++j) {
 		const uint32_t w = tid + j * PECH_MAIN_THREADS, k = w >> 8, e = w & 0xFFu;
-		const u32x4 v = (u32x4)(t128[j]);
+		const u32x4 v = (u32x4)(il ? t16k[j] : t128[j]);
 		char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
 #pragma unroll
 		for (uint32_t q = 0; q < 8u; ++q)
@@ -1187,7 +1279,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		uint32_t blk = 0;
 		// full blocks: every lane's rows valid, prefetch stays inside every run
 		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
-			const uint64_t base = S.ad + (uint64_t)blk * U * PECH_ROW_BYTES;
+			const uint64_t base = S.ad + (uint64_t)blk * U * rsb;
 #ifdef PECH_STAMPS
 			if (nstep == 0 && (blk == nblk / 4u || blk == nblk / 2u || blk == 3u * nblk / 4u))
 				tq[blk == nblk / 4u ? 0 : (blk == nblk / 2u ? 1 : 2)] = __builtin_amdgcn_s_memrealtime();
@@ -1200,55 +1292,55 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				// after it (half the lookahead); here a load waits only behind
 				// stores issued before it.  Measured: C3 copy 449-465 -> 389-397 us
 				// per launch (profiles/r02/ab_copy_block.txt).
-				ring[U - 1] = LD_PIECE(S, base + (U - 1) * PECH_ROW_BYTES, 2);
+				ring[U - 1] = LD_PIECE(S, base + (U - 1) * rsb, 2);
 #pragma unroll
 				for (uint32_t i = 0; i < U; ++i)
 					horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
 #pragma unroll
 				for (uint32_t i = 0; i < U; ++i)
-					st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_HEAD(S)));
+					st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_HEAD(S)), rsb);
 #pragma unroll
 				for (uint32_t i = 0; i + 1 < U; ++i)
-					ring[i] = LD_PIECE(S, base + (U + i) * PECH_ROW_BYTES, 2);
+					ring[i] = LD_PIECE(S, base + (U + i) * rsb, 2);
 				continue;
 			}
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
-				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
+				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * rsb, 2);
 				horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
-				st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_HEAD(S)));
+				st_piece<COPY>(S, blk * U + i, ring[i], S.nu != 0 && (i != 0 || blk != 0 || !STEP_HEAD(S)), rsb);
 			}
 		}
 		// ragged blocks: clamped prefetch, predicated update
 		for (; blk + 1 < nblk; ++blk) {
 			const uint32_t r = blk * U;
 			if constexpr (COPY) { // block discipline (see the full blocks), clamped and predicated
-				ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 3);
+				ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S), rsb), 3);
 #pragma unroll
 				for (uint32_t i = 0; i < U; ++i)
 					horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 #pragma unroll
 				for (uint32_t i = 0; i < U; ++i)
 					st_piece<COPY>(S, r + i, ring[i],
-						       r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i));
+						       r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i), rsb);
 #pragma unroll
 				for (uint32_t i = 0; i + 1 < U; ++i)
-					ring[i] = LD_PIECE(S, row_addr(S.ad, min(r + U + i, last), STEP_ZOFF(S)), 3);
+					ring[i] = LD_PIECE(S, row_addr(S.ad, min(r + U + i, last), STEP_ZOFF(S), rsb), 3);
 				continue;
 			}
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] =
-					LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S)), 3);
+					LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S), rsb), 3);
 				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 				st_piece<COPY>(S, r + i, ring[i],
-					       r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i));
+					       r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i), rsb);
 			}
 		}
 		// last block: its first load is this step's last row, the rest
 		// already fetch the next step's first rows
 		const uint32_t r = blk * U;
-		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S)), 4);
+		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S), rsb), 4);
 		uint32_t npos = S.pos, nlr = S.lr, nrem = S.rem;
 		if (jmax > 1u && nrem == 0) {
 			// item done: the next one from the pool (wave-uniform branch,
@@ -1270,7 +1362,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				}
 			}
 		}
-		const Step N = plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
+		const Step N = il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
+				  : plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
 		if constexpr (COPY) { // block discipline: this block's rows and stores, then the next step's loads
 			const bool more = N.T != 0;
 			const Step &L = more ? N : S;
@@ -1280,13 +1373,13 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i)
-				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i));
+				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i), rsb);
 #pragma unroll
 			for (uint32_t i = 1; i < U; ++i)
-				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
+				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L), rsb), 5);
 		} else {
 			horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
-			st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_HEAD(S)) && zl_keep(S, r));
+			st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_HEAD(S)) && zl_keep(S, r), rsb);
 			// Branch-free on purpose: with no next step the prefetch re-reads
 			// this step's last row (valid memory, never used).  An if/else here
 			// let LLVM sink the shared Horner code into a join block, which
@@ -1296,9 +1389,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			const uint32_t lrow0 = more ? 0u : last, lmax = more ? N.nl - 1u : last;
 #pragma unroll
 			for (uint32_t i = 1; i < U; ++i) {
-				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L)), 5);
+				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L), rsb), 5);
 				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
-				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && zl_keep(S, r + i));
+				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && zl_keep(S, r + i), rsb);
 			}
 		}
 #ifdef PECH_DEBUG_BOUNDS

@@ -46,6 +46,13 @@
 #ifndef PECH_ITEM_ROWS
 #define PECH_ITEM_ROWS 256u       /* uniform batches: rows per pooled work item */
 #endif
+#ifndef PECH_IL_COPY
+#define PECH_IL_COPY 0            /* fused copy's interleaved mode (A/B until measured on the GPU) */
+#endif
+#ifndef PECH_IL_MIN_ROWS
+#define PECH_IL_MIN_ROWS 1024u    /* fused copy: uniform batches of buffers this large walk interleaved rows */
+#endif
+#define PECH_IL_GROUPS 128u       /* lane groups of a main-kernel workgroup: the interleave stride in rows */
 #ifndef PECH_POOL_MIN_SHARE
 #define PECH_POOL_MIN_SHARE 1024u /* uniform batches pool only shares of at least this many rows */
 #endif
@@ -69,7 +76,8 @@
 #define PECH_C_POWB 5120u   /* x^(8*j*64^i), i<6, j<64     (byte shifts)      */
 #define PECH_C_TAB1 5504u   /* A_1 = the reference table, include/crc32c.h:16 */
 #define PECH_C_XINV 5760u   /* x^(-8k), k < 128 (trailing virtual zeros)      */
-#define PECH_C_WORDS 5888u
+#define PECH_C_TAB16K 5888u /* A_16384 byte tables (fused copy, interleaved rows) */
+#define PECH_C_WORDS 6912u
 
 /* device batch descriptor (matches struct crc32c_desc in include/) */
 struct pech_desc {

@@ -224,7 +224,57 @@ def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None):
     return out
 
 
-def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
+IL = C["PECH_IL_GROUPS"]
+IL_MIN = C["PECH_IL_MIN_ROWS"]
+
+
+def walk_il(cores, pos, lr, rem, U, events):
+    """Fused copy, interleaved rows (kernel plan_il): the workgroup's 128 lane
+    groups walk each portion [lr, lr + P) of a buffer together, group j taking
+    rows lr + j, lr + j + 128, ..."""
+    guard = 0
+    while rem:
+        guard += 1
+        assert guard < 10 ** 6
+        cd = cores[pos]
+        rows0 = cd["rows"]
+        P = min(rows0 - lr, rem)
+        for wave in range(WAVES_PER_WG):
+            j0 = 8 * wave
+            counts = [(P - j0 - g + IL - 1) // IL if P > j0 + g else 0 for g in range(8)]
+            T = counts[0]
+            nmin = min([c for c in counts if c] or [0])
+            for grp in range(8):
+                j, nn = j0 + grp, counts[grp]
+                st = lr + j
+                last = st + IL * (nn - 1)
+                for g8 in range(8):
+                    if nn:
+                        zoff = 16 * (cd["vp"] - g8) if (st == 0 and g8 < cd["vp"]) else 0
+                        loads, used = run_rows_loads(U, nn, nn, zoff, T, nmin)
+                        for row, z in loads:
+                            events.append(("load", cd, cd["vbase"] + (st + IL * row) * ROW + 16 * g8 + (zoff if z else 0)))
+                        zl = last == rows0 - 1 and g8 >= 8 - cd["zt"]
+                        zh = cd["zh"] if (st == 0 and g8 == cd["vp"]) else 0
+                        for row in used:
+                            events.append(("use", cd["orig"], st + IL * row, g8,
+                                           (zoff != 0 and row == 0) or (zl and row == nn - 1), zh if row == 0 else 0))
+                    else:  # idle group: the portion's first row, state ignored
+                        zoff = 16 * (cd["vp"] - g8) if (lr == 0 and g8 < cd["vp"]) else 0
+                        loads, _ = run_rows_loads(U, 1, 0, zoff, T, nmin)
+                        for row, z in loads:
+                            events.append(("load", cd, cd["vbase"] + (lr + IL * row) * ROW + 16 * g8 + (zoff if z else 0)))
+                if nn:
+                    events.append(("finish", cd["orig"], last + 1, (rows0 - last - 1) * ROW + cd["tail"] - 16 * cd["zt"]))
+        rem -= P
+        if lr + P == rows0:
+            pos += 1
+            lr = 0
+        else:
+            lr += P
+
+
+def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None, copy=False):
     """Yield events: ("load", buf, lane_piece_addr), ("use", orig, row, g8,
     virtual) and ("finish", orig, run_end_row, m) over every wave's range."""
     U = U or C["PECH_U"]
@@ -241,6 +291,13 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None):
     U0 = partials[0] // nz[0] if nz and nz[0] else 0
     uniform = bool(U0) and all((z & NZ_UNIFORM) and n * U0 == p for z, n, p in zip(nzs, nz, partials))
     ranges = wave_ranges(Rtot, ncu, rpw_min, weights)
+    if copy and uniform and U0 >= IL_MIN:  # fused copy: interleaved rows over each workgroup's range
+        for w0 in range(0, len(ranges), WAVES_PER_WG):
+            shares = ranges[w0:w0 + WAVES_PER_WG]
+            wg0, wg_rows = shares[0][0], shares[-1][1] - shares[0][0]
+            if wg_rows:
+                walk_il(cores, wg0 // U0, wg0 % U0, wg_rows, U, events)
+        return events
     for w0 in range(0, len(ranges), WAVES_PER_WG):
         shares = ranges[w0:w0 + WAVES_PER_WG]
         wg_rows = shares[-1][1] - shares[0][0]

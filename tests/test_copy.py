@@ -98,3 +98,26 @@ def test_copy_huge_buffer_misaligned(torch_dev):
     got, dst = run_copy(torch, dev, host, [3], [L], [11], L + 64, [0x12345678])
     assert int(got[0]) == O.crc(0x12345678, host[3:3 + L])
     check_copy(host, [3], [L], [11], dst)
+
+
+@pytest.mark.parametrize("size,n,soff,doff", [
+    (4 << 20, 37, 0, 0),                 # interleaved rows, ranges cut mid-buffer (37 over 256 workgroups)
+    ((1 << 17) + 5, 300, 3, 11),         # 1,025 rows each, unaligned sources and destinations
+    ((1 << 17) - 16, 513, 16, 1),        # just below and around the threshold of the mode
+    ((6 << 20) + 99, 3, 7, 0),           # few buffers, many workgroups each
+])
+def test_copy_uniform_large_buffers(torch_dev, size, n, soff, doff):
+    # uniform batches of large buffers take the fused copy's interleaved mode
+    # (the workgroup's 128 lane groups walk rows 128 apart, plan_il): every
+    # CRC and every destination byte, guards intact
+    torch, dev = torch_dev
+    rng = np.random.default_rng(size + n)
+    stride_s, stride_d = size + 4096, size + 8192
+    src_offs = soff + stride_s * np.arange(n, dtype=np.int64)  # the same alignment for every buffer: uniform
+    dst_offs = doff + stride_d * np.arange(n, dtype=np.int64)
+    lens = np.full(n, size, np.int64)
+    host = rng.integers(0, 256, int(src_offs[-1] + size + 64), dtype=np.uint8)
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64)
+    got, dst = run_copy(torch, dev, host, src_offs, lens, dst_offs, int(dst_offs[-1] + size + 4096), seeds)
+    assert np.array_equal(got, O.crcs(host, src_offs, lens, seeds))
+    check_copy(host, src_offs, lens, dst_offs, dst)

@@ -11,10 +11,10 @@ import pytest
 import kernel_model as KM
 
 
-def check(descs, ncu=4, seed=0, weights=None, U=None):
+def check(descs, ncu=4, seed=0, weights=None, U=None, copy=False):
     rng = random.Random(seed)
     cores, lrs, partials, nzs = KM.plan(descs, rng)
-    ev = KM.main(cores, lrs, partials, nzs, ncu, weights=weights, U=U)
+    ev = KM.main(cores, lrs, partials, nzs, ncu, weights=weights, U=U, copy=copy)
     used = collections.Counter()
     byorig = {}
     for c in cores:
@@ -152,3 +152,18 @@ def test_pool_min_share(monkeypatch, pool_min):
     monkeypatch.setattr(KM, "POOL_MIN", pool_min)
     check([(0x100000 * (i + 1), 1 << 16) for i in range(32)], ncu=2)
     check([(0x100000 * (i + 1), 1 << 20) for i in range(2)], ncu=2)
+
+
+@pytest.mark.parametrize("ncu,descs", [
+    (2, [(0x100000 * (i + 1), 1 << 20) for i in range(5)]),             # 8192-row buffers, ranges cut mid-buffer
+    (3, [(0x40000 * (i + 1) + 48, (1 << 17) - 48) for i in range(7)]),   # 1,024 rows, unaligned start, ragged portions
+    (1, [(0x1000 + 5, (3 << 20) + 777)]),                                 # one misaligned buffer over one workgroup
+])
+def test_fused_copy_interleaved_rows(ncu, descs):
+    # the fused copy's interleaved mode (plan_il): every core row consumed
+    # once by the lane group it belongs to, loads inside the buffer's lines,
+    # every run shifted to its buffer's end
+    cores, lrs, partials, nzs = KM.plan(descs)
+    assert all(z & KM.NZ_UNIFORM for z in nzs)
+    assert min(c["rows"] for c in cores if c is not None) >= KM.IL_MIN  # the interleaved mode, not the slices
+    check(descs, ncu=ncu, copy=True, U=12)
