@@ -47,7 +47,7 @@
 #define PECH_ITEM_ROWS 256u       /* uniform batches: rows per pooled work item */
 #endif
 #ifndef PECH_IL_COPY
-#define PECH_IL_COPY 0            /* fused copy's interleaved mode (A/B until measured on the GPU) */
+#define PECH_IL_COPY 1            /* fused copy's interleaved mode (profiles/r03/ab_copy_interleaved.txt) */
 #endif
 #ifndef PECH_IL_MIN_ROWS
 #define PECH_IL_MIN_ROWS 1024u    /* fused copy: uniform batches of buffers this large walk interleaved rows */
