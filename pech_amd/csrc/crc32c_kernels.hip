@@ -982,7 +982,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 	for (uint32_t j = 0; j < T128; ++j) {
 		t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
-		t16k[j] = COPY ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS] : 0u; // interleaved mode's table
+		t16k[j] = COPY || PECH_IL_CRC ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS] : 0u; // interleaved mode's table
 	}
 	u32x4 tv[TPT];
 #pragma unroll
@@ -1052,7 +1052,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		uok = uok && (uint64_t)(nc[k] & PECH_NZ_MASK) * U0 == (uint64_t)pc[k];
 	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
 	// fused copy of a uniform batch of large buffers: interleaved rows (plan_il)
-	const bool il = PECH_IL_COPY && COPY && uniform && U0 >= PECH_IL_MIN_ROWS;
+	const bool il = (COPY ? PECH_IL_COPY : PECH_IL_CRC) && uniform && U0 >= PECH_IL_MIN_ROWS;
 	const uint32_t rsb = il ? PECH_IL_GROUPS * PECH_ROW_BYTES : PECH_ROW_BYTES; // bytes from one row of a run to the next
 	STAMP(t_scan);
 	// Every wave gets an equal share of the batch's rows (at least rpw_min).
@@ -1090,7 +1090,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifdef PECH_NO_POOL // A/B: static shares for every batch
 	const uint32_t jmax = 0u;
 #else
-	const uint32_t jmax = !COPY && uniform && wg_rows >= PECH_MAIN_WAVES * PECH_POOL_MIN_SHARE
+	const uint32_t jmax = !COPY && !il && uniform && wg_rows >= PECH_MAIN_WAVES * PECH_POOL_MIN_SHARE
 				      ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
 										      PECH_MAIN_WAVES) + PECH_ITEM_ROWS - 1u) /
 							     PECH_ITEM_ROWS

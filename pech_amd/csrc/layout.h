@@ -49,6 +49,9 @@
 #ifndef PECH_IL_COPY
 #define PECH_IL_COPY 1            /* fused copy's interleaved mode (profiles/r03/ab_copy_interleaved.txt) */
 #endif
+#ifndef PECH_IL_CRC
+#define PECH_IL_CRC 0             /* the same for the CRC-only kernel (A/B: reads gained nothing in the probe) */
+#endif
 #ifndef PECH_IL_MIN_ROWS
 #define PECH_IL_MIN_ROWS 1024u    /* fused copy: uniform batches of buffers this large walk interleaved rows */
 #endif
