@@ -1649,7 +1649,6 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
 	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
 	const uint32_t wave = uni(tid >> 6);
-	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 	constexpr uint32_t T128 = 1024u / PECH_MAIN_THREADS;
 	constexpr uint32_t NT4 = (PECH_C_TAB1 - PECH_C_TAB4) / 4u;
 	constexpr uint32_t TPT = (NT4 + PECH_MAIN_THREADS - 1u) / PECH_MAIN_THREADS;
@@ -1665,12 +1664,31 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 	const uint32_t txi = consts[PECH_C_XINV + (tid & 127u)];
 	// the wave's positions: an equal split of the batch
 	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
+#ifndef PECH_DIRECT_WAVE_SHARES
+	// Workgroup-interleaved positions (v0.21): step k of wave w takes
+	// positions wb + 128 k + 8 w .. + 7 of the workgroup's range [wb, we), so
+	// the workgroup's 128 lane groups are on 128 consecutive buffers (one
+	// window per CU) and its waves end together; per launch equal, two-stream
+	// value +3-5 % (profiles/r03/ab_direct_wg_interleave.txt).
+	const uint32_t wb = (uint32_t)((uint64_t)blockIdx.x * n / gridDim.x);
+	const uint32_t we = (uint32_t)((uint64_t)(blockIdx.x + 1u) * n / gridDim.x);
+	uint32_t kstep = 0;
+	auto next_step = [&]() {
+		const uint32_t e0 = min(wb + 128u * kstep + 8u * wave + 8u, we);
+		uint32_t p = min(wb + 128u * kstep + 8u * wave, e0), ph0 = 0;
+		++kstep;
+		return plan_direct(descs, consts, p, e0, ph0, g8, grp);
+	};
+#else // A/B: each wave an equal share of the positions, in blocks of 16 (v0.17-v0.20)
+	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 	uint32_t pos = (uint32_t)((uint64_t)wglob * n / W), ph = 0;
 	const uint32_t pend = (uint32_t)((uint64_t)(wglob + 1u) * n / W);
+	auto next_step = [&]() { return plan_direct(descs, consts, pos, pend, ph, g8, grp); };
+#endif
 	// (spread over 128 lines of the table: one line for every wave was an L2 hot spot)
 	const uint64_t dummy = (uint64_t)consts + (uint64_t)((wglob * 8u + grp) & 127u) * PECH_ROW_BYTES + 16u * g8;
 	static_assert(128u * PECH_ROW_BYTES <= PECH_C_WORDS * 4u, "dummy lines inside the constants");
-	Step S = plan_direct(descs, consts, pos, pend, ph, g8, grp);
+	Step S = next_step();
 	u32x4 ring[U];
 	if (S.T)
 		RING_PRIME(S, ring);
@@ -1720,7 +1738,7 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 		}
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, dload_addr(S, r + U - 1, last, dummy), 4);
-		const Step N = plan_direct(descs, consts, pos, pend, ph, g8, grp);
+		const Step N = next_step();
 		// the last block's rows past every group's run (S.T, wave-uniform)
 		// are skipped by a scalar branch: their loads keep the ring's order
 		if (r < S.T)
@@ -1804,6 +1822,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.20 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.21 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved) lds-bank-replicated-A128 U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -828,6 +828,54 @@ __global__ __launch_bounds__(1024, 1) void k_wg_interleave(const uint8_t *p, uin
 		out[b] = pad[(threadIdx.x + 1u) & 1023u];
 }
 
+// Small buffers (4 KiB = 32 rows, one per lane group per step, as the CRC
+// kernels walk them): static shares (wave w takes buffers [w S, (w+1) S), 8
+// per step) or workgroup-interleaved (step k of wave w takes buffers
+// base + 128 k + 8 w .. + 7 of its workgroup's range: the workgroup's 128
+// groups are on 128 consecutive buffers, one 512 KiB window per step).
+template <bool COPY, bool IL>
+__global__ __launch_bounds__(1024, 1) void k_small(const uint8_t *p, uint8_t *q, uint32_t R, uint32_t *out)
+{
+	__shared__ uint32_t pad[36 * 1024];
+	constexpr uint32_t BR = 32u; // rows per buffer
+	const uint32_t wave = uni(threadIdx.x / 64u), lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+	const uint32_t nbuf = R / BR, G = gridDim.x;
+	const uint32_t b0 = (uint32_t)((uint64_t)nbuf * blockIdx.x / G), b1 = (uint32_t)((uint64_t)nbuf * (blockIdx.x + 1u) / G);
+	const uint32_t per = b1 - b0; // buffers of this workgroup
+	pad[threadIdx.x] = lane;
+	u32x4 acc = (u32x4)(0u), ring[D];
+	const uint32_t steps = (per + 127u) / 128u;
+	for (uint32_t k = 0; k < steps; ++k) {
+		uint32_t b;
+		bool ok;
+		if (IL) {
+			b = 128u * k + 8u * wave + grp;
+			ok = b < per;
+		} else {
+			const uint32_t ws = (per + 15u) / 16u; // the wave's share, 8 buffers per step
+			b = ws * wave + 8u * k + grp;
+			ok = 8u * k + grp < ws && b < per;
+		}
+		const uint32_t row0 = (b0 + (ok ? b : 0u)) * BR;
+		for (uint32_t r = 0; r < BR; r += D) {
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				ring[i] = ld(p, row0 + r + i, g8);
+#pragma unroll
+			for (int i = 0; i < D; ++i) {
+				if (COPY) {
+					if (ok)
+						__builtin_nontemporal_store(ring[i], (g_u32x4w *)(q + (uint64_t)(row0 + r + i) * ROW + 16u * g8));
+				} else {
+					acc ^= ring[i];
+				}
+			}
+		}
+	}
+	if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u)
+		out[blockIdx.x] = pad[(threadIdx.x + 1u) & 1023u];
+}
+
 // grid copy with one float4 per thread, workgroups of NT threads holding
 // PADW words of LDS (occupancy control)
 template <int NT, int PADW>
@@ -1421,6 +1469,32 @@ int main(int argc, char **argv)
 			}
 			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v],
 			       tot / reps * 1e3, 2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+	}
+	if (!strcmp(which, "small")) { // 4 KiB buffers (run with a 256 MiB size: the C2 batch)
+		const char *names[] = {"copy 4 KiB buffers, static shares", "copy 4 KiB buffers, workgroup-interleaved",
+				       "read 4 KiB buffers, static shares", "read 4 KiB buffers, workgroup-interleaved"};
+		for (int v = 0; v < 4; ++v) {
+			float tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				switch (v) {
+				case 0: hipLaunchKernelGGL((k_small<true, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 1: hipLaunchKernelGGL((k_small<true, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				case 2: hipLaunchKernelGGL((k_small<false, false>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				default: hipLaunchKernelGGL((k_small<false, true>), dim3(ncu), dim3(1024), 0, 0, src, buf[2], R, out); break;
+				}
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			const bool cp = v < 2;
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"%s\": %.1f}", sep(), names[v], tot / reps * 1e3,
+			       cp ? "GBps_read_plus_write" : "GBps", (cp ? 2.0 : 1.0) * bytes / (tot / reps * 1e-3) / 1e9);
 		}
 	}
 	if (!strcmp(which, "copyshape")) {
