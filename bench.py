@@ -124,7 +124,10 @@ def main():
     backend = os.environ.get("PECH_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local %= max(1, torch.cuda.device_count())
-    if world > 1:
+    # PECH_BENCH_FORCE_DIST=1: the process-group path at world size 1 too (a
+    # one-GPU rehearsal of the N>1 code on RCCL: init, barriers, MAX timing,
+    # device gather, per-rank parity)
+    if world > 1 or os.environ.get("PECH_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
 
         torch.cuda.set_device(local)

@@ -55,3 +55,21 @@ def test_torchrun_two_ranks_real_kernels():
     assert d["shards_checked"] == 2
     assert d["config"]["parallelism"].startswith("shard2")
     assert "cpu_baseline" not in d  # rank 0 at N=1 only
+
+
+def test_torchrun_rccl_process_group_one_rank():
+    """The driver's N>1 runs use RCCL (backend "nccl") with one GPU per rank,
+    which a one-GPU box cannot host for two ranks.  PECH_BENCH_FORCE_DIST=1
+    runs the same process-group code at world size 1 on RCCL: init with the
+    rank's device, barriers, the MAX all-reduce of the timing, the device
+    gather behind n_gpus and the per-rank parity reduction."""
+    env = dict(os.environ, PECH_BENCH_FORCE_DIST="1")
+    env.pop("PECH_BENCH_BACKEND", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "1", *COMMON],
+                       cwd=REPO, capture_output=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, lines
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["ranks"] == 1 and d["shards_checked"] == 1 and d["value"] > 0
