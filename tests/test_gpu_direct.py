@@ -70,9 +70,12 @@ def test_uniform_batches(torch_dev, P, size, skew):
     assert np.array_equal(got, O.crcs(buf.cpu().numpy(), offs, [size] * n))
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 15, 16, 17, 31, 33, 4095, 4097, 65537])
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 15, 16, 17, 31, 33, 255, 256, 257, 4095, 4097, 32767, 32769,
+                               65537, 98309])
 def test_position_splits(torch_dev, P, n):
-    # n below, at and across the wave count and the 16-position interleave
+    # n below, at and across the workgroup count (256), the workgroup step
+    # (128 positions per workgroup: 32,768 over the chip), the wave count and
+    # the 8-position steps
     torch, dev = torch_dev
     rng = np.random.default_rng(n)
     sizes = rng.integers(1, 9000, n)
