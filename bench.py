@@ -158,7 +158,7 @@ def main():
     batch_bytes = int(sizes.sum())
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     maxs = max(1, args.streams)
-    small_api = args.op == "crc" and (args.api == "small" or (args.api == "auto" and int(sizes.max()) < (32 << 10)))
+    small_api = args.api == "small" or (args.api == "auto" and int(sizes.max()) < (32 << 10))
 
     class Shard:
         """One device's batches: `rotate` distinct resident batches of random
@@ -193,7 +193,10 @@ def main():
 
         def step(self, i, k):
             with torch.cuda.device(self.dev):
-                if self.dsts:
+                if self.dsts and small_api:
+                    P.dev_copy_batch_small_async(self.descs[i % rotate], self.dsts[i % rotate][1],
+                                                 self.outs[i % rotate], stream=self.streams[k])
+                elif self.dsts:
                     P.dev_copy_batch_ws_async(self.descs[i % rotate], self.dsts[i % rotate][1],
                                               self.outs[i % rotate], self.wss[k], stream=self.streams[k])
                 elif small_api:
@@ -317,13 +320,13 @@ def main():
                                    f"{','.join(map(str, devids))}, no collective" if args.single_thread else
                                    f"shard{world} (independent buffers per GPU, no collective)"),
                    "streams": nstreams,
-                   "api": "crc32c_dev_batch_small_async" if small_api else
-                          ("crc32c_dev_copy_batch_ws_async" if dsts else "crc32c_dev_batch_ws_async"),
+                   "api": ("crc32c_dev_copy_batch_small_async" if dsts else "crc32c_dev_batch_small_async")
+                          if small_api else ("crc32c_dev_copy_batch_ws_async" if dsts else "crc32c_dev_batch_ws_async"),
                    "kernel": P.version()},
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "pech_crc32c_main_copy" if dsts else
-                               ("pech_crc32c_direct" if small_api else "pech_crc32c_main"),
+                     "kernel": ("pech_crc32c_direct_copy" if dsts else "pech_crc32c_direct") if small_api else
+                               ("pech_crc32c_main_copy" if dsts else "pech_crc32c_main"),
                      "bytes_per_launch": algo_bytes, "avg_launch_us": round(avg_kernel_s * 1e6, 2),
                      "launch_us_p10_p50_p90": [round(float(np.percentile(samples, q)), 2) for q in (10, 50, 90)]
                      if len(samples) else None,

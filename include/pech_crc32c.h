@@ -133,6 +133,12 @@ int crc32c_dev_copy_batch_async(const struct crc32c_desc *d_descs, const uint64_
 				unsigned int n, void *stream);
 int crc32c_dev_copy_batch_ws_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
 				   unsigned int n, void *d_workspace, size_t workspace_bytes, void *stream);
+/* Fused CRC + copy of a small-buffer batch: as crc32c_dev_copy_batch_async,
+ * in ONE launch with no workspace (the direct kernel, as
+ * crc32c_dev_batch_small_async: balanced for buffers below 32 KiB, correct
+ * for any; graph-capturable; d_out needs no initialisation). */
+int crc32c_dev_copy_batch_small_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
+				      unsigned int n, void *stream);
 
 /* Pre-size the internal workspace of the current device for n buffers. */
 int crc32c_dev_reserve(unsigned int n);

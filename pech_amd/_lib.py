@@ -50,6 +50,8 @@ SIGNATURES = {
     "crc32c_dev_copy_batch_ws_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                       ctypes.c_uint, ctypes.c_void_p, ctypes.c_size_t,
                                                       ctypes.c_void_p]),
+    "crc32c_dev_copy_batch_small_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_uint, ctypes.c_void_p]),
     "crc32c_shift": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
     "crc32c_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     "crc32c_device_init": (ctypes.c_int, []),

@@ -160,6 +160,21 @@ def dev_copy_batch_ws_async(descs, dsts, out, ws, stream=None):
                                                ws.numel(), stream.cuda_stream), "crc32c_dev_copy_batch_ws_async")
 
 
+def dev_copy_batch_small_async(descs, dsts, out, stream=None):
+    """Fused CRC + copy of a small-buffer batch (crc32c_dev_copy_batch_small_async):
+    one launch of the direct kernel, no workspace; balanced for buffers below
+    32 KiB, correct for any."""
+    import torch
+
+    n = descs.shape[0]
+    if out.numel() < n or out.element_size() != 4 or dsts.numel() < n or dsts.element_size() != 8:
+        raise ValueError("out must hold n 32-bit words, dsts n 64-bit addresses")
+    if stream is None:
+        stream = torch.cuda.current_stream(descs.device)
+    check(lib().crc32c_dev_copy_batch_small_async(descs.data_ptr(), dsts.data_ptr(), out.data_ptr(), n,
+                                                  stream.cuda_stream), "crc32c_dev_copy_batch_small_async")
+
+
 def crc32c_tensors(tensors, seeds=None, offsets=None, lengths=None):
     """CRCs of device uint8 tensors (optionally sub-ranges [off, off+len)).
     Synchronous convenience wrapper; returns a list of ints."""

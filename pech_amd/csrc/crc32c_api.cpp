@@ -38,7 +38,7 @@ extern "C" hipError_t pech_launch_main(uint32_t, const pech_ws *, const uint32_t
 
 extern "C" const char *pech_kernel_tag(void);
 extern "C" hipError_t pech_launch_direct(const pech_desc *, uint32_t, const uint32_t *, uint32_t *, uint32_t,
-					 hipStream_t, hipEvent_t, hipEvent_t);
+					 hipStream_t, hipEvent_t, hipEvent_t, const uint64_t *);
 extern "C" hipError_t pech_launch_small(const void *, uint32_t, uint32_t, const uint32_t *, uint32_t *, uint32_t,
 					hipStream_t);
 
@@ -319,7 +319,8 @@ static int launch_internal_ws(DevCtx *c, const pech_desc *d_descs, uint32_t *d_o
 
 // The direct kernel (no plan kernel, no workspace): small-buffer batches,
 // in launches of at most PECH_MAX_BATCH descriptors (output slots are 20 bits)
-static int launch_small(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, hipStream_t stream)
+static int launch_small(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, hipStream_t stream,
+			const uint64_t *d_dsts = nullptr)
 {
 	for (unsigned int off = 0; off < n; off += PECH_MAX_BATCH) {
 		const unsigned int m = (n - off) < PECH_MAX_BATCH ? (n - off) : PECH_MAX_BATCH;
@@ -333,7 +334,8 @@ static int launch_small(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 				HIP_TRY(hipEventCreate(&tl.b));
 			}
 		}
-		HIP_TRY(pech_launch_direct(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, stream, tl.a, tl.b));
+		HIP_TRY(pech_launch_direct(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, stream, tl.a, tl.b,
+					   d_dsts ? d_dsts + off : nullptr));
 		if (g_timing)
 			c->pending.push_back(tl);
 	}
@@ -1043,6 +1045,25 @@ int crc32c_dev_copy_batch_async(const struct crc32c_desc *d_descs, const uint64_
 		if (rc)
 			return rc;
 		return launch_internal_ws(c, (const pech_desc *)d_descs, d_out, n, (hipStream_t)stream, d_dsts);
+	});
+}
+
+int crc32c_dev_copy_batch_small_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
+				      unsigned int n, void *stream)
+{
+	if (n == 0)
+		return 0;
+	if (!d_descs || !d_dsts || !d_out) {
+		set_err("crc32c_dev_copy_batch_small_async: invalid arguments");
+		return -EINVAL;
+	}
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		DevCtx *c = nullptr;
+		int rc = ctx_get(&c);
+		if (rc)
+			return rc;
+		return launch_small(c, (const pech_desc *)d_descs, d_out, n, (hipStream_t)stream, d_dsts);
 	});
 }
 

@@ -36,6 +36,9 @@
 #ifndef PECH_U
 #define PECH_U 8 // rows in flight per lane
 #endif
+#ifndef PECH_U_DCOPY
+#define PECH_U_DCOPY 8 // rows per block, direct fused copy (block discipline; 12 spills there)
+#endif
 #ifndef PECH_U_COPY
 #define PECH_U_COPY 12 // rows per block, fused-copy variant (block discipline, 128 VGPRs)
 #endif
@@ -1511,8 +1514,10 @@ __device__ __forceinline__ u32x4 tail_keep(const Step &S, uint32_t row, u32x4 v)
 // blocks of 16 (group g takes pos + 2g, then pos + 2g + 1: for buffers laid
 // out back to back every group walks one contiguous 2-buffer range, as the
 // plan kernel's order does), a plain run of up to 8 at the range's end.
+template <bool COPY = false>
 __device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs, const uint32_t *consts,
-					    uint32_t &pos, uint32_t end, uint32_t &ph, uint32_t g8, uint32_t grp)
+					    uint32_t &pos, uint32_t end, uint32_t &ph, uint32_t g8, uint32_t grp,
+					    const uint64_t *__restrict__ dsts = nullptr)
 {
 	Step S;
 	S.T = 0;
@@ -1536,6 +1541,7 @@ __device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs,
 	const uint32_t cnt = il ? 8u : min(left, 8u);
 	// one descriptor per group by scalar loads (wave-uniform addresses)
 	uint32_t alo = 0, ahi = 0, len = 0, seed = 0;
+	uint64_t dst = 0;
 #pragma unroll
 	for (uint32_t j = 0; j < 8; ++j) {
 		const uint32_t pj = il ? pos + 2u * j + ph : pos + min(j, cnt - 1u);
@@ -1545,6 +1551,8 @@ __device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs,
 		ahi = mine ? uni((uint32_t)(dj.addr >> 32)) : ahi;
 		len = mine ? uni(dj.len) : len;
 		seed = mine ? uni(dj.seed) : seed;
+		if (COPY)
+			dst = mine ? uni64(dsts[pj]) : dst;
 	}
 	const uint32_t b = il ? pos + 2u * grp + ph : pos + grp;
 	const bool have = grp < cnt;
@@ -1593,8 +1601,34 @@ __device__ __forceinline__ Step plan_direct(const pech_desc *__restrict__ descs,
 	} else {
 		pos += cnt;
 	}
-	S.dad = S.ad;
+	// fused copy: this lane's row-0 piece in the destination (a source byte
+	// at a goes to a + dst - addr); groups without rows store nothing
+	S.dad = COPY && rows ? S.ad + (dst - addr) : S.ad;
 	return S;
+}
+
+// Direct fused copy: the bytes of row `row`'s piece that are the buffer's
+// go to the destination -- a whole 16-byte store, or, for the partial pieces
+// at the buffer's two ends (bytes before it in row 0, past it in the last
+// row), byte stores.  Pieces wholly outside the buffer and rows past the run
+// store nothing.
+template <bool COPY>
+__device__ __forceinline__ void st_direct(const Step &S, uint32_t row, u32x4 v)
+{
+	typedef __attribute__((address_space(1))) u32x4 g_u32x4w;
+	if (!COPY || row >= S.nu)
+		return;
+	const uint32_t lo = row == 0u ? (STEP_ZOFF(S) ? 16u : STEP_ZH(S)) : 0u;
+	const uint32_t hi = row == S.nu - 1u ? DSTEP_KB(S) : 16u;
+	const uint64_t a = S.dad + (uint64_t)row * PECH_ROW_BYTES;
+	if (lo == 0u && hi == 16u) {
+		__builtin_nontemporal_store(v, (g_u32x4w *)a);
+		return;
+	}
+#pragma unroll
+	for (uint32_t i = 0; i < 16u; ++i)
+		if (i >= lo && i < hi)
+			*(__attribute__((address_space(1))) uint8_t *)(a + i) = (uint8_t)(v[i >> 2] >> (8u * (i & 3u)));
 }
 
 // Direct mode: fold as finish_run, undo the trailing zeros, add the seed's
@@ -1641,9 +1675,10 @@ __device__ __forceinline__ uint64_t dload_addr(const Step &S, uint32_t row, uint
 #endif
 }
 
-template <uint32_t U>
+template <uint32_t U, bool COPY = false>
 __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__restrict__ descs, uint32_t n,
-					    const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
+					    const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+					    const uint64_t *__restrict__ dsts = nullptr)
 {
 	const uint32_t tid = threadIdx.x;
 	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
@@ -1677,13 +1712,13 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 		const uint32_t e0 = min(wb + 128u * kstep + 8u * wave + 8u, we);
 		uint32_t p = min(wb + 128u * kstep + 8u * wave, e0), ph0 = 0;
 		++kstep;
-		return plan_direct(descs, consts, p, e0, ph0, g8, grp);
+		return plan_direct<COPY>(descs, consts, p, e0, ph0, g8, grp, dsts);
 	};
 #else // A/B: each wave an equal share of the positions, in blocks of 16 (v0.17-v0.20)
 	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 	uint32_t pos = (uint32_t)((uint64_t)wglob * n / W), ph = 0;
 	const uint32_t pend = (uint32_t)((uint64_t)(wglob + 1u) * n / W);
-	auto next_step = [&]() { return plan_direct(descs, consts, pos, pend, ph, g8, grp); };
+	auto next_step = [&]() { return plan_direct<COPY>(descs, consts, pos, pend, ph, g8, grp, dsts); };
 #endif
 	// (spread over 128 lines of the table: one line for every wave was an L2 hot spot)
 	const uint64_t dummy = (uint64_t)consts + (uint64_t)((wglob * 8u + grp) & 127u) * PECH_ROW_BYTES + 16u * g8;
@@ -1722,6 +1757,19 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 		uint32_t blk = 0;
 		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
 			const uint64_t base = S.ad + (uint64_t)blk * U * PECH_ROW_BYTES;
+			if constexpr (COPY) { // block discipline, as the main copy kernel (vmcnt counts stores in order)
+				ring[U - 1] = LD_PIECE(S, base + (U - 1) * PECH_ROW_BYTES, 2);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					horner_row(lds, lreg, ring[i], s0, s1, s2, s3);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					st_direct<COPY>(S, blk * U + i, ring[i]);
+#pragma unroll
+				for (uint32_t i = 0; i + 1 < U; ++i)
+					ring[i] = LD_PIECE(S, base + (U + i) * PECH_ROW_BYTES, 2);
+				continue;
+			}
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] = LD_PIECE(S, base + (i + U - 1) * PECH_ROW_BYTES, 2);
@@ -1730,6 +1778,19 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 		}
 		for (; blk + 1 < nblk; ++blk) {
 			const uint32_t r = blk * U;
+			if constexpr (COPY) {
+				ring[U - 1] = LD_PIECE(S, dload_addr(S, r + U - 1, last, dummy), 3);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					horner_row_pred(lds, lreg, tail_keep(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+#pragma unroll
+				for (uint32_t i = 0; i < U; ++i)
+					st_direct<COPY>(S, r + i, ring[i]);
+#pragma unroll
+				for (uint32_t i = 0; i + 1 < U; ++i)
+					ring[i] = LD_PIECE(S, dload_addr(S, r + U + i, last, dummy), 3);
+				continue;
+			}
 #pragma unroll
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] = LD_PIECE(S, dload_addr(S, r + i + U - 1, last, dummy), 3);
@@ -1739,6 +1800,25 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, dload_addr(S, r + U - 1, last, dummy), 4);
 		const Step N = next_step();
+		if constexpr (COPY) { // this block's rows and stores, then the next step's first loads
+			const bool more = N.T != 0;
+			const Step &L = more ? N : S;
+			const uint32_t lmax = more ? N.nl - 1u : last;
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i)
+				if (r + i < S.T)
+					horner_row_pred(lds, lreg, tail_keep(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+#pragma unroll
+			for (uint32_t i = 0; i < U; ++i)
+				if (r + i < S.T)
+					st_direct<COPY>(S, r + i, ring[i]);
+#pragma unroll
+			for (uint32_t i = 1; i < U; ++i)
+				ring[i - 1] = LD_PIECE(L, dload_addr(L, more ? i - 1 : lmax + 1u, lmax, dummy), 5);
+			finish_direct(lds, g8, s0, s1, s2, s3, S, descs, out);
+			S = N;
+			continue;
+		}
 		// the last block's rows past every group's run (S.T, wave-uniform)
 		// are skipped by a scalar branch: their loads keep the ring's order
 		if (r < S.T)
@@ -1763,6 +1843,16 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_d
 {
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	direct_body<PECH_U>(lds, descs, n, consts, out);
+}
+
+// fused CRC + copy of a small-buffer batch (crc32c_dev_copy_batch_small_async):
+// the direct kernel with every consumed piece also stored to its destination
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_direct_copy(
+	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	const uint64_t *__restrict__ dsts)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
+	direct_body<PECH_U_DCOPY, true>(lds, descs, n, consts, out, dsts);
 }
 
 // ---- host-side launchers (used by crc32c_api.cpp) -------------------------
@@ -1809,12 +1899,18 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 	return hipGetLastError();
 }
 
-// direct kernel (no plan, no workspace); ev_start/ev_stop as pech_launch_main
+// direct kernel (no plan, no workspace); ev_start/ev_stop as pech_launch_main;
+// dsts != NULL: the fused-copy variant
 extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, const uint32_t *consts, uint32_t *out,
-					 uint32_t ncu, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)
+					 uint32_t ncu, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop,
+					 const uint64_t *dsts)
 {
-	hipExtLaunchKernelGGL(pech_crc32c_direct, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u,
-			      descs, n, consts, out);
+	if (dsts)
+		hipExtLaunchKernelGGL(pech_crc32c_direct_copy, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start,
+				      ev_stop, 0u, descs, n, consts, out, dsts);
+	else
+		hipExtLaunchKernelGGL(pech_crc32c_direct, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop,
+				      0u, descs, n, consts, out);
 	return hipGetLastError();
 }
 

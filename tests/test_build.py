@@ -41,7 +41,8 @@ def kernel_body(asm, name):
 
 
 @pytest.mark.parametrize("kernel", ["pech_crc32c_plan", "pech_crc32c_main", "pech_crc32c_plan_copy",
-                                    "pech_crc32c_main_copy", "pech_crc32c_small", "pech_crc32c_direct"])
+                                    "pech_crc32c_main_copy", "pech_crc32c_small", "pech_crc32c_direct",
+                                    "pech_crc32c_direct_copy"])
 def test_no_calls_no_scratch(device_asm, kernel):
     asm, _ = device_asm
     body = kernel_body(asm, kernel)
@@ -49,7 +50,8 @@ def test_no_calls_no_scratch(device_asm, kernel):
     assert "scratch_" not in body and "buffer_store_dword" not in body, "register spill"
 
 
-@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct"])
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct",
+                                    "pech_crc32c_direct_copy"])
 def test_main_kernel_register_budget(device_asm, kernel):
     _, remarks = device_asm
     m = re.search(r"Function Name: %s \[.*?VGPRs: (\d+).*?ScratchSize \[bytes/lane\]: (\d+)" % kernel, remarks,

@@ -20,7 +20,7 @@ def torch_dev():
     return torch, torch.device("cuda:0")
 
 
-def run_copy(torch, dev, host_src, src_offs, lens, dst_offs, dst_bytes, seeds=None):
+def run_copy(torch, dev, host_src, src_offs, lens, dst_offs, dst_bytes, seeds=None, small=False):
     import pech_amd as P
     from pech_amd import _lib
 
@@ -29,9 +29,12 @@ def run_copy(torch, dev, host_src, src_offs, lens, dst_offs, dst_bytes, seeds=No
     descs = P.make_descs(src.data_ptr() + np.asarray(src_offs, dtype=np.int64), lens, seeds, device=dev)
     dsts = torch.from_numpy((dst.data_ptr() + np.asarray(dst_offs, dtype=np.int64)).astype(np.int64)).to(dev)
     out = torch.zeros(len(lens), dtype=torch.int32, device=dev)
-    rc = _lib.lib().crc32c_dev_copy_batch_async(descs.data_ptr(), dsts.data_ptr(), out.data_ptr(), len(lens),
-                                                 torch.cuda.current_stream(dev).cuda_stream)
-    _lib.check(rc, "crc32c_dev_copy_batch_async")
+    fn = "crc32c_dev_copy_batch_small_async" if small else "crc32c_dev_copy_batch_async"
+    if small:  # the direct kernel stores its results: out must need no initialisation
+        out.fill_(-1)
+    rc = getattr(_lib.lib(), fn)(descs.data_ptr(), dsts.data_ptr(), out.data_ptr(), len(lens),
+                                 torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(rc, fn)
     torch.cuda.synchronize()
     return out.cpu().numpy().view(np.uint32), dst.cpu().numpy()
 
@@ -46,13 +49,15 @@ def check_copy(host_src, src_offs, lens, dst_offs, got_dst):
     assert np.all(outside == GUARD), f"{int(np.count_nonzero(outside != GUARD))} bytes written outside destinations"
 
 
-def test_copy_random_unaligned(torch_dev):
+@pytest.mark.parametrize("small", [False, True])
+def test_copy_random_unaligned(torch_dev, small):
     # random lengths (tiny ones included), sources and destinations at
-    # unrelated byte alignments, gaps between destinations to catch stray writes
+    # unrelated byte alignments, gaps between destinations to catch stray
+    # writes; small: the one-launch direct copy (crc32c_dev_copy_batch_small_async)
     torch, dev = torch_dev
     rng = np.random.default_rng(77)
     n = 1500
-    lens = rng.integers(0, 70000, n)
+    lens = rng.integers(0, 70000 if not small else 40000, n)
     tiny = rng.random(n) < 0.15
     lens[tiny] = rng.integers(0, 40, int(tiny.sum()))
     src_offs, dst_offs = np.zeros(n, np.int64), np.zeros(n, np.int64)
@@ -65,7 +70,30 @@ def test_copy_random_unaligned(torch_dev):
         dp += int(lens[i])
     host = rng.integers(0, 256, sp + 64, dtype=np.uint8)
     seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64)
-    got, dst = run_copy(torch, dev, host, src_offs, lens, dst_offs, dp + 64, seeds)
+    got, dst = run_copy(torch, dev, host, src_offs, lens, dst_offs, dp + 64, seeds, small=small)
+    assert np.array_equal(got, O.crcs(host, src_offs, lens, seeds))
+    check_copy(host, src_offs, lens, dst_offs, dst)
+
+
+@pytest.mark.parametrize("n,maxlen", [(1, 5), (7, 33), (300, 200), (4097, 4200), (70000, 5000)])
+def test_copy_small_api_shapes(torch_dev, n, maxlen):
+    # the direct copy over tiny to messenger-sized buffers, every length mod
+    # 16 and every source/destination alignment mix, counts across the
+    # workgroup and 128-position steps
+    torch, dev = torch_dev
+    rng = np.random.default_rng(n * 31 + maxlen)
+    lens = rng.integers(0, maxlen + 1, n)
+    src_offs, dst_offs = np.zeros(n, np.int64), np.zeros(n, np.int64)
+    sp = dp = 0
+    for i in range(n):
+        sp += int(rng.integers(0, 33))
+        dp += int(rng.integers(1, 33))
+        src_offs[i], dst_offs[i] = sp, dp
+        sp += int(lens[i])
+        dp += int(lens[i])
+    host = rng.integers(0, 256, sp + 64, dtype=np.uint8)
+    seeds = np.where(rng.random(n) < 0.5, 0, rng.integers(0, 1 << 32, n)).astype(np.uint64)
+    got, dst = run_copy(torch, dev, host, src_offs, lens, dst_offs, dp + 64, seeds, small=True)
     assert np.array_equal(got, O.crcs(host, src_offs, lens, seeds))
     check_copy(host, src_offs, lens, dst_offs, dst)
 
