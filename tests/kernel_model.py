@@ -444,3 +444,24 @@ def walk(cores, nzs, pos, lr, rem, U, events, grid=False):
                     pos += kcut
                     lr = 0
     return events
+
+
+def direct_positions(n, ncu, waves=None):
+    """The direct kernel's schedule (v0.21, workgroup-interleaved): workgroup
+    b owns positions [b n / ncu, (b+1) n / ncu); step k of its wave w takes
+    positions wb + 128 k + 8 w + g (g < 8, below the range end), one per
+    lane group.  Yields (workgroup, wave, step, group, position)."""
+    waves = waves or WAVES_PER_WG
+    for b in range(ncu):
+        wb, we = b * n // ncu, (b + 1) * n // ncu
+        for w in range(waves):
+            k = 0
+            while True:
+                e0 = min(wb + 128 * k + 8 * w + 8, we)
+                p = min(wb + 128 * k + 8 * w, e0)
+                if p >= e0:  # the kernel's S.T == 0: no later step has positions either
+                    assert wb + 128 * (k + 1) + 8 * w >= we
+                    break
+                for g in range(min(8, e0 - p)):
+                    yield b, w, k, g, p + g
+                k += 1

@@ -167,3 +167,12 @@ def test_fused_copy_interleaved_rows(ncu, descs):
     assert all(z & KM.NZ_UNIFORM for z in nzs)
     assert min(c["rows"] for c in cores if c is not None) >= KM.IL_MIN  # the interleaved mode, not the slices
     check(descs, ncu=ncu, copy=True, U=12)
+
+
+@pytest.mark.parametrize("n,ncu", [(1, 256), (7, 256), (255, 256), (256, 256), (257, 256), (4097, 256),
+                                   (32767, 256), (32769, 256), (65536, 256), (98309, 256), (1000, 3)])
+def test_direct_kernel_positions_once(n, ncu):
+    # the direct kernel's workgroup-interleaved schedule: every position of
+    # the batch taken by exactly one lane group, in steps of <= 8 per wave
+    seen = collections.Counter(p for *_, p in KM.direct_positions(n, ncu))
+    assert sorted(seen) == list(range(n)) and set(seen.values()) == {1}
