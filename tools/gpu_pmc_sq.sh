@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 CFG=${CFG:-c3}
-BENCH="bench.py --no-cpu-baseline --no-host-path --streams 1 --config $CFG --steps 10 --warmup 2 --sustain-seconds 0"
+BENCH="bench.py --no-cpu-baseline --no-host-path --streams 1 --config $CFG --op ${OP:-crc} --steps 10 --warmup 2 --sustain-seconds 0"
 i=0
 for PMC in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"; do
