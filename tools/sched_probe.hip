@@ -968,6 +968,54 @@ __global__ __launch_bounds__(256) void k_copy_gridk(const uint8_t *p, uint8_t *q
 			__builtin_nontemporal_store(v[k], (g_u32x4w *)(q + 16u * (b + 256u * k)));
 }
 
+// The grid copy carrying a stand-in for a per-tile partial CRC:
+// 256-thread workgroups, one float4 per thread (4 KiB tile), TABW words of
+// tables filled into LDS per workgroup from global memory (L2-resident), 16
+// byte lookups per thread (dependent for TABW < 4096, slice-by-16 otherwise),
+// a 6-round cross-lane fold with 4 lookups a round, one partial per wave.
+template <int TABW>
+__global__ __launch_bounds__(256) void k_copy_tilecrc(const uint8_t *p, uint8_t *q, uint64_t n16, const uint32_t *tab,
+						      uint32_t *part)
+{
+	__shared__ uint32_t t[TABW];
+	for (uint32_t k = threadIdx.x; k < (uint32_t)TABW; k += 256u)
+		t[k] = tab[k];
+	const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+	const u32x4 v = __builtin_nontemporal_load((g_u32x4 *)(p + 16u * min(i, n16 - 1u)));
+	if (i < n16)
+		__builtin_nontemporal_store(v, (g_u32x4w *)(q + 16u * i));
+	__syncthreads();
+	const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+	uint32_t c = 0;
+#pragma unroll
+	for (int j = 0; j < 16; ++j) {
+		const uint32_t b = (w4[j >> 2] >> (8 * (j & 3))) & 255u;
+		if (TABW >= 4096)
+			c ^= t[(15 - j) * 256 + b];
+		else
+			c = t[((c ^ b) & 255u) | ((j & (TABW / 256 - 1)) << 8)] ^ (c >> 8);
+	}
+	for (int off = 1; off < 64; off <<= 1) {
+		const uint32_t o = __shfl_xor(c, off);
+		c = o ^ t[c & 255u] ^ t[((c >> 8) & 255u) | (256u % TABW)] ^ t[((c >> 16) & 255u) | (512u % TABW)] ^
+		    t[(c >> 24) | (768u % TABW)];
+	}
+	if ((threadIdx.x & 63u) == 0 && i < n16)
+		part[i >> 6] = c;
+}
+
+// folds 64 consecutive partials into one word (the batch's second launch)
+__global__ __launch_bounds__(256) void k_tile_fold(const uint32_t *part, uint64_t nout, uint32_t *out)
+{
+	const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+	if (i >= nout)
+		return;
+	uint32_t c = 0;
+	for (int k = 0; k < 64; ++k)
+		c = (c << 1 | c >> 31) ^ part[64u * i + k];
+	out[i] = c;
+}
+
 // Static shares for the first ncu workgroups over rows [0, Rs), then X
 // extra workgroups over [Rs, R) in equal pieces: the dispatcher hands each
 // extra workgroup to the first CU whose static workgroup has exited (one
@@ -1576,6 +1624,46 @@ int main(int argc, char **argv)
 				break;
 			}
 		}
+	}
+	if (!strcmp(which, "tilecrc")) { // can the grid copy carry a per-tile CRC?
+		const char *names[] = {"copy grid 1 float4/thread", "tile copy + CRC stand-in, 1 KiB table, dependent lookups",
+				       "tile copy + CRC stand-in, 4 KiB tables, dependent lookups",
+				       "tile copy + CRC stand-in, 16 KiB tables, slice-by-16",
+				       "tile copy + CRC stand-in, 4 KiB tables, + fold launch"};
+		const uint64_t n16 = bytes / 16, nparts = n16 / 64 + 1, nout = n16 / 64 / 64;
+		uint32_t *tab, *part, *fold;
+		CHECK(hipMalloc(&tab, 4096 * 4));
+		CHECK(hipMemset(tab, 0x5a, 4096 * 4));
+		CHECK(hipMalloc(&part, nparts * 4));
+		CHECK(hipMalloc(&fold, (nout + 1) * 4));
+		const int nv = (int)(sizeof(names) / sizeof(names[0]));
+		for (int v = 0; v < nv; ++v) {
+			float tot = 0;
+			for (int r = -2; r < reps; ++r) {
+				CHECK(hipEventRecord(e0, 0));
+				const uint8_t *src = buf[(r + 4) % 2];
+				const dim3 g((unsigned)(n16 / 256));
+				switch (v) {
+				case 0: hipLaunchKernelGGL((k_copy_gridk<1>), g, dim3(256), 0, 0, src, buf[2], n16); break;
+				case 1: hipLaunchKernelGGL((k_copy_tilecrc<256>), g, dim3(256), 0, 0, src, buf[2], n16, tab, part); break;
+				case 3: hipLaunchKernelGGL((k_copy_tilecrc<4096>), g, dim3(256), 0, 0, src, buf[2], n16, tab, part); break;
+				default: hipLaunchKernelGGL((k_copy_tilecrc<1024>), g, dim3(256), 0, 0, src, buf[2], n16, tab, part); break;
+				}
+				if (v == 4)
+					hipLaunchKernelGGL(k_tile_fold, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, 0, part, nout, fold);
+				CHECK(hipEventRecord(e1, 0));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				if (r >= 0)
+					tot += ms;
+			}
+			printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps_read_plus_write\": %.1f}", sep(), names[v], tot / reps * 1e3,
+			       2.0 * bytes / (tot / reps * 1e-3) / 1e9);
+		}
+		CHECK(hipFree(tab));
+		CHECK(hipFree(part));
+		CHECK(hipFree(fold));
 	}
 	if (all || !strcmp(which, "window")) {
 		const char *names[] = {"read tiles 8 KiB (drifting)", "read tiles 8 KiB, WG lockstep",
