@@ -12,8 +12,11 @@ LIB = pech_amd/libpech_crc32c.so
 HOST_OBJ = build/crc32c_api.o build/crc32c_async.o build/crc32c_cpu.o build/crc32c_msgr.o
 OBJ = build/crc32c_kernels.o $(HOST_OBJ)
 
+# the reference sources exist in the build container only (never on the GPU box)
+REF_PRESENT := $(wildcard /root/reference/src/ceph/messenger.c)
+
 all: $(LIB) oracle build/msgr_sim build/msgr_conn_sim build/dropin_kat build/coro_stack build/dropin_bench build/launch_cost \
-     build/lib_dbg.so build/lib_test.so build/hbm_probe build/sched_probe
+     build/lib_dbg.so build/lib_test.so build/hbm_probe build/sched_probe $(if $(REF_PRESENT),build/msgr_loopback)
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -86,6 +89,15 @@ build/msgr_conn_sim: tests/c/msgr_conn_sim.c oracle/crc32c_oracle.c include/pech
 	@mkdir -p build
 	gcc -std=gnu89 -O2 -Wall -Werror -Iinclude tests/c/msgr_conn_sim.c oracle/crc32c_oracle.c -Lpech_amd \
 		-lpech_crc32c -Wl,-rpath,'$$ORIGIN/../pech_amd' -o $@
+
+# test program (built in the build container, run on both sides): the
+# reference messenger ITSELF, patched by integration/pech_crc32c_msgr.patch
+# in a temp dir, linked with all of pech but main.c and with the library;
+# tests/c/msgr_loopback.c is only its caller (tests/test_msgr_loopback.py)
+build/msgr_loopback: tests/c/msgr_loopback.c tests/c/loopback_proxy.c tests/c/loopback_proxy.h tests/pech_build.py \
+		     integration/pech_crc32c_msgr.patch oracle/crc32c_oracle.c include/pech_crc32c_msgr.h $(LIB)
+	@mkdir -p build
+	python3 tests/pech_build.py loopback $@
 
 # test program: the drop-in crc32c() from C, as messenger.c calls it
 build/dropin_kat: tests/c/dropin_kat.c include/crc32c.h $(LIB)

@@ -94,9 +94,12 @@ unsigned int crc32c_msgr_set_host_max(unsigned int bytes);
  * or on the host up to crc32c_msgr_set_host_max()) and compared with
  * footer_crc; otherwise the message is ready at once.  msg may be NULL with
  * check == 0: an in-order marker for a message the messenger skipped, so
- * in_seq still advances in arrival order.  The messenger must not modify or
- * free data until msg is returned by rx_next or released.  0, -EAGAIN
- * (queue full: stop reading, dispatch first), or < 0. */
+ * in_seq still advances in arrival order.  Markers are always taken, and
+ * consecutive ones share one entry (a count), so the queue holds at most
+ * 2 * max_pending + 1 entries however many messages are skipped while its
+ * head waits.  The messenger must not modify or free data until
+ * msg is returned by rx_next or released.  0, -EAGAIN (queue full: stop
+ * reading, dispatch first), or < 0. */
 int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data, unsigned int len, int check,
 			 uint32_t footer_crc);
 

@@ -417,14 +417,14 @@ static int reap(crc32c_async *a, bool wait_oldest, DeviceGuard *dg = nullptr)
 				if (s->finished.load(std::memory_order_seq_cst))
 					break;
 				q = hipStreamQuery(s->stream);
+				if (q == hipSuccess && s->inject_fail)
+					q = hipErrorLaunchFailure; // test build: as a failed stream reports itself
 				if (q != hipSuccess && q != hipErrorNotReady)
 					break; // failed: its host function will not run
 				(void)hipGetLastError();
 				q = hipSuccess; // (done but not yet marked: the flag comes next)
 			}
 			s->waiting.store(0, std::memory_order_relaxed);
-			if (q == hipSuccess && s->inject_fail)
-				q = hipErrorLaunchFailure; // test build: as a failed stream reports itself
 		} else if (!s->finished.load(std::memory_order_acquire)) {
 			// a failed stream never runs its host function: ask the stream,
 			// once the batch has had kQueryAfterNs to finish (complete() is

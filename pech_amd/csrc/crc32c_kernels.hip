@@ -482,9 +482,9 @@ extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
 // step), and the wave's cursor after the step.
 struct Step {
 	uint64_t ad;
-	uint32_t mp;  // rows after the run << 7 | zt << 4 | tail   (m = 128 rows + tail - 16 zt)
+	uint32_t mp;  // rows after the run << 7 | zt << 4 | tail   (m = 128 rows + tail - 16 zt; mp_bits)
 	uint32_t nl, nu;
-	uint32_t oz;  // orig | (zoff / 16) << 20 | zh << 23 | zl << 27   (zoff <= 112, zh < 16)
+	uint32_t oz;  // orig | (zoff / 16) << 20 | zh << 23 | zl << 27 | ra bit 25 << 29   (zoff <= 112, zh < 16)
 	uint32_t T, nmin;
 	uint32_t pos, lr, rem;
 	uint64_t dad; // fused copy: destination of this lane's piece in row 0 (ad + dst - src)
@@ -524,6 +524,9 @@ __device__ __forceinline__ u32x4 ld_piece(uint64_t a, uint64_t lo, uint64_t hi, 
 #endif
 
 static_assert(PECH_MAIN_WAVES % 4 == 0 && PECH_MAIN_WAVES <= 16, "waves per workgroup: 4, 8, 12 or 16");
+// the interleaved fused copy's row stride and the direct kernel's position
+// stride are the workgroup's lane groups: one constant for both
+static_assert(PECH_IL_GROUPS == PECH_GROUP_LANES * PECH_MAIN_WAVES, "PECH_IL_GROUPS = 8 groups x PECH_MAIN_WAVES");
 
 // Step.oz bits of lane g8 when its run starts at the buffer's row 0 (first):
 // lb leading bytes of the row lie before the buffer -- pieces below lb/16
@@ -542,6 +545,17 @@ __device__ __forceinline__ uint32_t tail_bits(bool last, uint32_t g8, uint32_t z
 {
 	return last && g8 >= 8u - zt ? 1u << 27 : 0u;
 }
+
+// Step.mp of a run with `ra` rows of its buffer after it: ra << 7 | zt << 4 |
+// tail.  ra reaches 2^25 (a core of 2^25 + 1 rows: a buffer within 255 bytes
+// of 4 GiB, whose first row is a run of its own), which wraps 32 bits after
+// the shift, so bit 25 of ra goes to Step.oz bit 29 (ra_bit) -- ADVICE r3.
+#define PECH_OZ_RA25 (1u << 29)
+__device__ __forceinline__ uint32_t mp_bits(uint32_t ra, uint32_t meta)
+{
+	return (ra << 7) | (meta >> 16 & 0x70u) | PECH_META_TAIL(meta);
+}
+__device__ __forceinline__ uint32_t ra_bit(uint32_t ra) { return (ra >> 25 & 1u) << 29; }
 
 // v with its bytes [0, kb) kept and [kb, 16) zeroed (0 <= kb <= 16)
 __device__ __forceinline__ u32x4 keep_below(u32x4 v, uint32_t kb)
@@ -617,9 +631,9 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			S.ad = vb0 + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
 			S.nl = nn;
 			S.nu = nn;
-			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) |
+			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) | ra_bit(rows0 - st - nn) |
 			       tail_bits(st + nn == rows0, g8, zt0); // the first / this slice ends the buffer
-			S.mp = ((rows0 - st - nn) << 7) | (meta0 >> 16 & 0x70u) | PECH_META_TAIL(meta0);
+			S.mp = mp_bits(rows0 - st - nn, meta0);
 			S.T = q + (rm ? 1u : 0u);
 			S.nmin = q;
 			if (COPY)
@@ -712,7 +726,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			if (nu) {
 				S.ad = myvb + (uint64_t)mylr * PECH_ROW_BYTES + 16u * g8;
 				S.nl = nu;
-				S.oz = PECH_META_ORIG(my.meta) | head_bits(mylr == 0, g8, mylb) |
+				S.oz = PECH_META_ORIG(my.meta) | head_bits(mylr == 0, g8, mylb) | ra_bit(myrows - mylr - nu) |
 				       tail_bits(mylr + nu == myrows, g8, myzt); // the run ends the buffer
 			} else {
 				// idle groups reload group 0's rows (valid memory: the redirect
@@ -723,7 +737,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			}
 			S.nu = nu;
 			dl = mdl;
-			S.mp = ((myrows - mylr - nu) << 7) | (my.meta >> 16 & 0x70u) | PECH_META_TAIL(my.meta);
+			S.mp = mp_bits(myrows - mylr - nu, my.meta);
 #ifdef PECH_DEBUG_BOUNDS
 			const uint64_t bv = nu ? myvb : vb0;
 			S.blo = bv + 16u * ((nu ? mylb : lb0) >> 4);
@@ -795,8 +809,9 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 			S.ad = vb0 + (uint64_t)st * PECH_ROW_BYTES + 16u * g8;
 			S.nl = nn;
 			S.nu = nn;
-			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) | tail_bits(last == rows0 - 1u, g8, zt0);
-			S.mp = ((rows0 - last - 1u) << 7) | (meta0 >> 16 & 0x70u) | PECH_META_TAIL(meta0);
+			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) | ra_bit(rows0 - last - 1u) |
+			       tail_bits(last == rows0 - 1u, g8, zt0);
+			S.mp = mp_bits(rows0 - last - 1u, meta0);
 		} else {
 			// an idle group reloads the portion's first row (valid memory,
 			// the redirect of row 0's pieces before the buffer kept), ignored
@@ -828,8 +843,9 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 #define STEP_ORIG(S) ((S).oz & 0xFFFFFu)
 #define STEP_ZH(S) (((S).oz >> 23) & 15u)
 #define STEP_HEAD(S) (((S).oz >> 20) & 0x7Fu) // row 0's piece is not wholly the buffer's (zoff or zh)
-#define STEP_ZL(S) ((S).oz & (1u << 27)) // bit 28: STEP_SLOW (direct kernel)
-#define STEP_M(S) ((int64_t)((uint64_t)((S).mp >> 7) * PECH_ROW_BYTES + ((S).mp & 15u)) - (int64_t)((S).mp & 0x70u))
+#define STEP_ZL(S) ((S).oz & (1u << 27)) // bit 28: STEP_SLOW (direct kernel), bit 29: PECH_OZ_RA25
+#define STEP_RA(S) ((uint64_t)((S).mp >> 7) | (uint64_t)((S).oz & PECH_OZ_RA25) >> 4) // rows after the run
+#define STEP_M(S) ((int64_t)(STEP_RA(S) * PECH_ROW_BYTES + ((S).mp & 15u)) - (int64_t)((S).mp & 0x70u))
 
 // Ring discipline: row k of a step lives in ring slot k % PECH_U and the
 // lookahead is PECH_U-1 rows.  The iteration that consumes row k first issues
@@ -1709,8 +1725,8 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 	const uint32_t we = (uint32_t)((uint64_t)(blockIdx.x + 1u) * n / gridDim.x);
 	uint32_t kstep = 0;
 	auto next_step = [&]() {
-		const uint32_t e0 = min(wb + 128u * kstep + 8u * wave + 8u, we);
-		uint32_t p = min(wb + 128u * kstep + 8u * wave, e0), ph0 = 0;
+		const uint32_t e0 = min(wb + PECH_IL_GROUPS * kstep + 8u * wave + 8u, we);
+		uint32_t p = min(wb + PECH_IL_GROUPS * kstep + 8u * wave, e0), ph0 = 0;
 		++kstep;
 		return plan_direct<COPY>(descs, consts, p, e0, ph0, g8, grp, dsts);
 	};

@@ -43,6 +43,7 @@ struct rx_ent {
 	unsigned int len;
 	uint32_t want, got;
 	int state, check;
+	unsigned int skips; /* a marker (msg NULL): the consecutive skipped messages it stands for */
 };
 
 struct tx_ent {
@@ -179,6 +180,14 @@ int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data
 		return -EINVAL;
 	if (c->npending >= c->max_pending && msg) /* skip markers hold no message: always taken */
 		return -EAGAIN;
+	if (!msg && c->tail && !c->tail->msg) {
+		/* consecutive markers share an entry: entries stay bounded by
+		 * 2 * max_pending + 1 while the head waits for its CRC */
+		c->tail->skips++;
+		c->npending++;
+		g_st.rx_unchecked++;
+		return 0;
+	}
 	e = rx_alloc(c);
 	if (!e)
 		return -ENOMEM;
@@ -189,6 +198,7 @@ int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data
 	e->len = len;
 	e->want = footer_crc;
 	e->check = check != 0;
+	e->skips = msg ? 0u : 1u;
 	e->state = e->check ? ST_WAIT : ST_DONE;
 	if (c->tail)
 		c->tail->next = e;
@@ -226,6 +236,13 @@ int crc32c_msgr_rx_next(struct crc32c_msgr_conn *c, void **msg, uint32_t *crc)
 	e = c->head;
 	if (!e || e->state != ST_DONE)
 		return 0;
+	if (!e->msg && e->skips > 1) { /* one skipped message of a shared marker */
+		e->skips--;
+		c->npending--;
+		*msg = NULL;
+		*crc = 0u;
+		return 1;
+	}
 	c->head = e->next;
 	if (!c->head)
 		c->tail = NULL;

@@ -55,7 +55,9 @@
 #ifndef PECH_IL_MIN_ROWS
 #define PECH_IL_MIN_ROWS 1024u    /* fused copy: uniform batches of buffers this large walk interleaved rows */
 #endif
-#define PECH_IL_GROUPS 128u       /* lane groups of a main-kernel workgroup: the interleave stride in rows */
+#ifndef PECH_IL_GROUPS
+#define PECH_IL_GROUPS 128u       /* lane groups of a main-kernel workgroup (8 x waves): the interleave stride */
+#endif
 #ifndef PECH_POOL_MIN_SHARE
 #define PECH_POOL_MIN_SHARE 1024u /* uniform batches pool only shares of at least this many rows */
 #endif

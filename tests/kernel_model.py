@@ -61,6 +61,18 @@ def core_rows(addr, ln):
     return ((addr & 127) + (ce - addr) + 127) >> 7
 
 
+def encode_m(ra, zt, tail):
+    """kernel mp_bits / ra_bit: (Step.mp, Step.oz bit) of a run with `ra` rows
+    of its buffer after it, in 32-bit words"""
+    return ((ra << 7) | (zt << 4) | tail) & 0xFFFFFFFF, ((ra >> 25) & 1) << 29
+
+
+def decode_m(mp, oz):
+    """kernel STEP_M: bytes from the run's end to the buffer's end"""
+    ra = (mp >> 7) | ((oz & (1 << 29)) >> 4)
+    return ra * ROW + (mp & 15) - (mp & 0x70)
+
+
 def size_class(rows):
     if rows >= LARGE:
         return 12

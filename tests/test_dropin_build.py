@@ -18,75 +18,16 @@ container only: /root/reference does not exist on the GPU box).
   the library.
 
 Nothing is written under /root/reference and no object is kept."""
-import glob
 import os
-import shutil
 import subprocess
 import tempfile
-from concurrent.futures import ThreadPoolExecutor
 
 import pytest
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REF = "/root/reference"
-LIBDIR = os.path.join(REPO, "pech_amd")
+import pech_build as B
+from pech_build import LIBDIR, PATCH, REF, REPO, build_pech_osd, compile_one, patched_tree
 
-pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "src", "ceph")),
-                                reason="needs the reference sources (build container only)")
-
-# the reference Makefile's CFLAGS (Makefile:2-12); gcc 11 also needs
-# unused-result demoted (include/random.h:10) and _FORTIFY_SOURCE off for
-# pech's cross-stack longjmp (SURVEY.md §8(c))
-CFLAGS = ["-g", "-O2", "-std=gnu89", "-Wall", "-Wdeclaration-after-statement", "-Wno-format", "-Werror",
-          "-Werror=date-time", "-Werror=incompatible-pointer-types", "-Werror=designated-init",
-          "-Wno-unused-const-variable", "-Wno-unused-but-set-variable", "-Wno-pointer-sign", "-fno-strict-aliasing",
-          "-fstack-protector-strong", "-Wno-error=unused-result", "-U_FORTIFY_SOURCE", "-D_FORTIFY_SOURCE=0",
-          "-D_GNU_SOURCE", "-D__KERNEL__"]
-
-
-PATCH = os.path.join(REPO, "integration", "pech_crc32c_msgr.patch")
-PATCHED = ("src/ceph/messenger.c", "include/ceph/messenger.h", "src/ceph/osd_server.c")
-
-
-def compile_one(src, obj, with_dropin=True, extra_inc=()):
-    inc = ((["-I" + os.path.join(REPO, "include")] if with_dropin else []) + ["-I" + d for d in extra_inc] +
-           ["-I" + os.path.join(REF, "include")])
-    return subprocess.run(["gcc", "-c", *CFLAGS, *inc, src, "-o", obj], capture_output=True, text=True, timeout=300)
-
-
-def patched_tree(d):
-    """Temp copies of the files the patch touches, patched; returns their root."""
-    root = os.path.join(d, "pech")
-    for rel in PATCHED:
-        os.makedirs(os.path.dirname(os.path.join(root, rel)), exist_ok=True)
-        shutil.copy(os.path.join(REF, rel), os.path.join(root, rel))
-    r = subprocess.run(["patch", "-p1", "--no-backup-if-mismatch", "-d", root, "-i", PATCH], capture_output=True,
-                       text=True, timeout=60)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "fuzz" not in r.stdout and "offset" not in r.stdout, r.stdout  # applies exactly
-    return root
-
-
-def build_pech_osd(d, root=None):
-    """Every src/**/*.c of pech compiled one by one into d (the patched copies
-    from `root` in place of the originals), linked against the library."""
-    srcs = sorted(glob.glob(os.path.join(REF, "src", "**", "*.c"), recursive=True))
-    assert len(srcs) > 30
-    if root:
-        srcs = [os.path.join(root, os.path.relpath(s, REF)) if os.path.relpath(s, REF) in PATCHED else s
-                for s in srcs]
-    extra = [os.path.join(root, "include")] if root else []
-    objs = [os.path.join(d, os.path.basename(os.path.dirname(s)) + "_" + os.path.basename(s)[:-2] + ".o")
-            for s in srcs]
-    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
-        res = list(ex.map(lambda so: compile_one(*so, extra_inc=extra), zip(srcs, objs)))
-    bad = [(s, r.stderr[-800:]) for s, r in zip(srcs, res) if r.returncode]
-    assert not bad, bad[:2]
-    exe = os.path.join(d, "pech-osd")
-    r = subprocess.run(["gcc", "-o", exe, *objs, "-L" + LIBDIR, "-lpech_crc32c", "-Wl,-rpath," + LIBDIR,
-                        "-lresolv", "-ldl", "-rdynamic"], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    return exe
+pytestmark = pytest.mark.skipif(not B.have_reference(), reason="needs the reference sources (build container only)")
 
 
 def bindings(exe):

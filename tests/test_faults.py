@@ -240,6 +240,61 @@ def sc_failed_stream_found_by_complete():
     ac.close()
 
 
+def sc_failed_stream_found_by_drain():
+    # the BLOCKING wait (drain, destroy) on a batch whose
+    # stream failed -- its host function never runs, so `finished` is never
+    # set -- must see the failure from the stream query and end
+    import pech_amd as P
+
+    d = np.random.default_rng(48).integers(0, 256, 10000, dtype=np.uint8)
+    ac = P.AsyncCrc()
+    got = []
+    inject(SITE_ASYNC_STREAM, 1)
+    ac.submit(d.ctypes.data, d.size, 5, lambda crc, err: got.append((crc, err)), keep=d)
+    ac.flush()
+    try:
+        ac.drain()
+        raise AssertionError("drain over a failed stream returned 0")
+    except P.Crc32cError:
+        pass
+    assert len(got) == 1 and got[0][1] < 0
+    assert ac.pending() == 0 and ac.stray == 0
+    ac.close()
+
+
+def sc_failed_stream_found_by_blocked_submit():
+    # ... and the submit that must wait for a free slot while every slot is
+    # in flight and the oldest one's stream failed: an error return for it
+    # (no callback), err < 0 for the failed slot's payload, exact CRCs for
+    # the slots that ran
+    import oracle_lib as O
+    import pech_amd as P
+
+    rng = np.random.default_rng(49)
+    bufs = [rng.integers(0, 256, 3000 + i, dtype=np.uint8) for i in range(5)]
+    ac = P.AsyncCrc()
+    got = {}
+    cb = lambda i: (lambda crc, err: got.__setitem__(i, (crc, err)))  # noqa: E731
+    inject(SITE_ASYNC_STREAM, 1)  # the first launch's stream "fails"
+    for i in range(4):  # four slots in flight (kMaxSlots)
+        ac.submit(bufs[i].ctypes.data, bufs[i].size, i, cb(i), keep=bufs[i])
+        ac.flush()
+    try:
+        ac.submit(bufs[4].ctypes.data, bufs[4].size, 4, cb(4), keep=bufs[4])
+        raise AssertionError("a submit blocked on a failed slot returned 0")
+    except P.Crc32cError:
+        pass
+    try:
+        ac.drain()
+    except P.Crc32cError:
+        pass  # the context's error is sticky
+    assert got[0][1] < 0
+    for i in (1, 2, 3):
+        assert got[i] == (O.crc(i, bufs[i]), 0), (i, got.get(i))
+    assert 4 not in got and ac.pending() == 0 and ac.stray == 0
+    ac.close()
+
+
 def sc_context_after_failure_is_replaceable():
     # a fresh context works after one failed (the failure is per context)
     import oracle_lib as O

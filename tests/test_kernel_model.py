@@ -39,6 +39,7 @@ def check(descs, ncu=4, seed=0, weights=None, U=None, copy=False):
             _, orig, endrow, m = e
             c = byorig[orig]
             assert m == (c["rows"] - endrow) * KM.ROW + c["tail"] - 16 * c["zt"]
+            assert KM.decode_m(*KM.encode_m(c["rows"] - endrow, c["zt"], c["tail"])) == m  # the kernel's packing
     for orig, c in byorig.items():
         for row in range(c["rows"]):
             for g8 in range(8):
@@ -176,3 +177,20 @@ def test_direct_kernel_positions_once(n, ncu):
     # the batch taken by exactly one lane group, in steps of <= 8 per wave
     seen = collections.Counter(p for *_, p in KM.direct_positions(n, ncu))
     assert sorted(seen) == list(range(n)) and set(seen.values()) == {1}
+
+
+def test_final_shift_packing_at_maximum_length():
+    # a buffer within 255 bytes of 4 GiB has a core of 2^25 + 1
+    # rows; a 1-row run at its start has 2^25 rows after it, which wraps the
+    # 32-bit Step.mp after its << 7 -- bit 25 rides in Step.oz bit 29
+    for addr in (127, 0x1000 + 113, 0x7F):
+        for ln in ((1 << 32) - 1, (1 << 32) - 17, (1 << 32) - 128):
+            rows = KM.core_rows(addr, ln)
+            ce = (addr + ln) & ~15
+            zt = rows * 8 - ((ce - (addr & ~127)) >> 4)
+            tail = addr + ln - ce
+            for ra in (0, 1, (1 << 25) - 1, rows - 1):
+                mp, oz = KM.encode_m(ra, zt, tail)
+                assert mp < 1 << 32
+                assert KM.decode_m(mp, oz) == ra * KM.ROW + tail - 16 * zt, (addr, ln, ra)
+    assert KM.core_rows(127, (1 << 32) - 1) == (1 << 25) + 1  # the case exists
