@@ -69,15 +69,20 @@ struct crc32c_async;
  * err < 0 if the GPU work failed (crc is then 0 and must not be used). */
 typedef void (*crc32c_done_fn)(void *arg, uint32_t crc, int err);
 
-/* flags for crc32c_async_create() */
+/* flags for crc32c_async_create().
+ * Default (0): payloads in crc32c_pages memory are read by the kernel in
+ * place over the host link: no H2D copy and no per-payload DMA call, so the
+ * caller's thread pays about a microsecond per payload at any size
+ * (DESIGN.md 6.4).  Pageable payloads are packed into pinned staging. */
 #define CRC32C_ASYNC_DEFAULT 0u
-/* payloads in crc32c_pages memory are read by the kernel in place over the
- * host link: no H2D copy and no per-payload DMA call, so the caller's thread
- * pays well under a microsecond per payload at any size.  Without the flag,
- * pinned payloads from 32 KiB up are DMA'd to device slots: more link
- * bandwidth for large payloads (MI355X: 42-50 vs 36-37 GiB/s at 1-4 MiB)
- * at 5-85 us of the caller's CPU per payload. */
+/* The default since round 4; accepted for callers written before. */
 #define CRC32C_ASYNC_ZEROCOPY 1u
+/* crc32c_pages payloads from 32 KiB up are DMA'd to device staging instead:
+ * more host-link bandwidth for large payloads (MI355X: 42-50 against 36-37
+ * GiB/s at 1-4 MiB) for more of the caller's CPU.  The copies are recorded
+ * at submit and issued together when the slot launches (one batched call
+ * where the HIP runtime has hipMemcpyBatchAsync).  Not with ZEROCOPY. */
+#define CRC32C_ASYNC_DMA 2u
 
 /* A context on the current device: its own HIP stream, staging slots and
  * eventfd.  NULL on failure.  Every later call on the context runs on that
@@ -91,7 +96,8 @@ struct crc32c_async *crc32c_async_create(unsigned int flags);
 int crc32c_async_fd(const struct crc32c_async *a);
 
 /* Queue crc32c(seed, buf, len) of HOST memory `buf` (pageable, or
- * crc32c_pages memory: DMA'd or read in place, no CPU copy).  The caller
+ * crc32c_pages memory: read in place, or DMA'd with CRC32C_ASYNC_DMA; no CPU
+ * copy).  The caller
  * keeps `buf` unchanged and alive until `done` runs (hold a ceph_msg_get()
  * reference, messenger.c:3907-3924).  Any length < 2^32, including 0.  A
  * full batch is launched automatically; otherwise call crc32c_async_flush(). */

@@ -269,10 +269,12 @@ class AsyncCrc:
     """crc32c_async context (include/pech_crc32c_async.h): submit host
     payloads, poll fd() from an event loop, complete() runs the callbacks."""
 
-    def __init__(self, zerocopy=False):
+    def __init__(self, dma=False):
+        """dma=False: crc32c_pages payloads are read in place (the default);
+        dma=True: CRC32C_ASYNC_DMA, DMA'd to device staging at launch."""
         from ._lib import DONE_FN
 
-        self._h = lib().crc32c_async_create(1 if zerocopy else 0)
+        self._h = lib().crc32c_async_create(2 if dma else 0)
         if not self._h:
             raise Crc32cError(f"crc32c_async_create failed: {lib().crc32c_last_error().decode()}")
         self._keep = {}  # submission key -> (payload ref, python callback)

@@ -4,17 +4,19 @@
 // Data path of one async context (up to four staging slots in flight, each
 // with its own HIP stream and workspace, so small batches overlap):
 //   submit()   places the payload in the slot being filled -- pageable bytes
-//              and crc32c_pages payloads below 32 KiB are packed into the
-//              slot's pinned staging buffer (one CPU copy, one H2D per slot),
-//              larger crc32c_pages payloads are DMA'd straight from where
-//              they lie (or, with CRC32C_ASYNC_ZEROCOPY, read by the kernel
-//              in place over the host link) -- and records one descriptor
-//              per piece.  A payload larger than what a slot has left is cut
-//              into pieces; piece 0 carries the seed, later pieces seed 0.
-//   flush()    H2D of the packed staging runs, plan + main kernels (the plan
-//              reads the descriptors in place from pinned memory), D2H of the
-//              results, and a host function that marks the slot finished and
-//              bumps the eventfd -- four stream operations per batch.
+//              are packed into the slot's pinned staging buffer (one CPU
+//              copy, one H2D per slot); crc32c_pages payloads are read by
+//              the kernel in place over the host link (the default), or,
+//              with CRC32C_ASYNC_DMA, packed below 32 KiB and DMA'd from
+//              where they lie above (copies recorded here, issued at the
+//              slot's launch) -- and records one descriptor per piece.
+//              A payload larger than what a slot has left is cut into
+//              pieces; piece 0 carries the seed, later pieces seed 0.
+//   flush()    DMA of the recorded payloads and H2D of the packed staging
+//              runs, plan + main kernels (the plan reads the descriptors in
+//              place from pinned memory), D2H of the results, and a host
+//              function that marks the slot finished and bumps the eventfd
+//              -- four stream operations per batch.
 //   complete() harvests finished slots in launch order, folds each piece
 //              into its payload (crc <- crc32c_combine(crc, piece, len)),
 //              frees the slot, and runs the callbacks of finished payloads
@@ -35,6 +37,7 @@
 // crc32c_async_pending() > 0 (include/pech_crc32c_async.h).
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
 #include <errno.h>
 #include <limits.h>
 #include <linux/futex.h>
@@ -227,10 +230,11 @@ struct DeviceGuard {
 };
 
 constexpr size_t kSlotBytes = 32u << 20; // staging per slot
-// CRC32C_ASYNC_ZEROCOPY reads every pinned payload in place.  Until round 3
-// payloads from 1 MiB up were DMA'd even then: a little more link bandwidth
-// (42-50 against 36-37 GiB/s), but 5-40 us of the caller's CPU per payload
-// against 0.6 (profiles/r03/ab_zc_max.txt); pech's one thread is the budget.
+// Zero-copy (the default since round 4) reads every pinned payload in place.
+// Until round 3 payloads from 1 MiB up were DMA'd even then: a little more
+// link bandwidth (42-50 against 36-37 GiB/s), but 5-40 us of the caller's
+// CPU per payload against 0.6 (profiles/r03/ab_zc_max.txt); pech's one
+// thread is the budget.
 constexpr size_t kZeroCopyMax = SIZE_MAX;
 // DMA mode: pinned payloads below this are packed into the slot's staging by
 // memcpy (one H2D per slot) instead of one hipMemcpyAsync each: a DMA call
@@ -248,6 +252,27 @@ struct Piece {
 	uint32_t len;
 };
 
+// CRC32C_ASYNC_DMA: a payload copy recorded at submit, issued at launch
+struct DmaCopy {
+	void *dst;
+	void *src;
+	size_t bytes;
+};
+
+// hipMemcpyBatchAsync (HIP 7.1+): one call for a slot's copies.  Resolved at
+// run time: a process may have loaded an older HIP runtime first (PyTorch
+// bundles its own), and the library must still load there.
+typedef hipError_t (*batch_copy_fn)(void **, void **, size_t *, size_t, hipMemcpyAttributes *, size_t *, size_t,
+				   size_t *, hipStream_t);
+static batch_copy_fn batch_copy()
+{
+	static const batch_copy_fn f = [] {
+		const char *e = getenv("PECH_ASYNC_DMA_BATCH"); // =0: one call per copy (A/B)
+		return e && e[0] == '0' ? nullptr : (batch_copy_fn)dlsym(RTLD_DEFAULT, "hipMemcpyBatchAsync");
+	}();
+	return f;
+}
+
 struct Slot {
 	hipStream_t stream = nullptr; // own stream and workspace: up to kMaxSlots batches overlap
 	void *d_ws = nullptr;
@@ -260,6 +285,7 @@ struct Slot {
 	int efd = -1;                 // the context's eventfd
 	std::vector<Piece> pieces;
 	std::vector<std::pair<size_t, size_t>> packed; // staging runs filled by memcpy: [lo, hi)
+	std::vector<DmaCopy> dma;                      // CRC32C_ASYNC_DMA payload copies, issued at launch
 	size_t used = 0;     // staging bytes
 	size_t zc_bytes = 0; // bytes read in place: a slot launches at kSlotBytes of either
 	uint32_t maxlen = 0; // longest piece: the direct kernel takes slots of pieces below kDirectMax
@@ -395,6 +421,7 @@ static void harvest(crc32c_async *a, Slot *s, int err)
 	}
 	s->pieces.clear();
 	s->packed.clear();
+	s->dma.clear();
 	s->used = 0;
 	s->zc_bytes = 0;
 	s->maxlen = 0;
@@ -503,6 +530,36 @@ static int launch_slot(crc32c_async *a)
 	if (!s || s->pieces.empty())
 		return 0;
 	const unsigned m = (unsigned)s->pieces.size();
+	if (!s->dma.empty()) {
+		hipError_t e = hipErrorInvalidValue;
+		if (!pech_fault(PECH_FAULT_ASYNC_DMA)) {
+			e = hipErrorNotSupported;
+			if (batch_copy_fn bc = batch_copy()) {
+				std::vector<void *> dsts, srcs;
+				std::vector<size_t> sizes;
+				for (const DmaCopy &c : s->dma) {
+					dsts.push_back(c.dst);
+					srcs.push_back(c.src);
+					sizes.push_back(c.bytes);
+				}
+				size_t fail_idx = 0;
+				e = bc(dsts.data(), srcs.data(), sizes.data(), dsts.size(), nullptr, nullptr, 0, &fail_idx,
+				       s->stream);
+			}
+			if (e != hipSuccess) { // no batched call in this runtime (or it refused): one call each
+				(void)hipGetLastError();
+				e = hipSuccess;
+				for (const DmaCopy &c : s->dma)
+					if ((e = hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyHostToDevice, s->stream)) !=
+					    hipSuccess)
+						break;
+			}
+		}
+		if (e != hipSuccess) {
+			pech_internal_set_err("crc32c_async: payload DMA failed: %s", hipGetErrorString(e));
+			return fail_cur_slot(a, -EIO);
+		}
+	}
 	for (auto &r : s->packed)
 		TRY_HIP(hipMemcpyAsync(s->d_stage + r.first, s->h_stage + r.first, r.second - r.first,
 				       hipMemcpyHostToDevice, s->stream),
@@ -537,8 +594,9 @@ static int launch_slot(crc32c_async *a)
 
 static struct crc32c_async *async_create(unsigned int flags)
 {
-	if (flags & ~CRC32C_ASYNC_ZEROCOPY) {
-		pech_internal_set_err("crc32c_async_create: unknown flags %#x", flags);
+	if ((flags & ~(CRC32C_ASYNC_ZEROCOPY | CRC32C_ASYNC_DMA)) ||
+	    (flags & (CRC32C_ASYNC_ZEROCOPY | CRC32C_ASYNC_DMA)) == (CRC32C_ASYNC_ZEROCOPY | CRC32C_ASYNC_DMA)) {
+		pech_internal_set_err("crc32c_async_create: invalid flags %#x", flags);
 		return nullptr;
 	}
 	if (crc32c_device_init())
@@ -583,14 +641,15 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 			crc32c_done_fn done, void *arg)
 {
 	// one registry lookup: pinned pages are read in place (zero-copy, below
-	// kZeroCopyMax) or DMA'd
+	// kZeroCopyMax) or, with CRC32C_ASYNC_DMA, DMA'd
 	const uint64_t dv = len ? pinned_dev_addr(buf, len) : 0;
-	const uint64_t zc = (a->flags & CRC32C_ASYNC_ZEROCOPY) && len < a->zc_max ? dv : 0;
+	const uint64_t zc = !(a->flags & CRC32C_ASYNC_DMA) && len < a->zc_max ? dv : 0;
 	const bool dma = !zc && dv != 0 && len >= kDmaMin;
-	// the common case needs no HIP call: one descriptor into the open slot,
-	// which it does not fill
+	// the common case needs no HIP call: one descriptor (and, with
+	// CRC32C_ASYNC_DMA, one recorded copy) into the open slot, which it does
+	// not fill
 	const Slot *c = a->cur;
-	const bool quiet = c && !dma && c->pieces.size() + 1u < kSlotDescs && (zc ? c->zc_bytes + len < kSlotBytes : c->used + len + 512u < kSlotBytes);
+	const bool quiet = c && c->pieces.size() + 1u < kSlotDescs && (zc ? c->zc_bytes + len < kSlotBytes : c->used + len + 512u < kSlotBytes);
 	DeviceGuard dg(a->dev, !quiet);
 	if (!quiet && !dg.ok) {
 		pech_internal_set_err("crc32c_async_submit: cannot select device %d", a->dev);
@@ -630,15 +689,9 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 			piece = left < kSlotBytes - s->used ? left : kSlotBytes - s->used;
 			d.addr = (uint64_t)(uintptr_t)(s->d_stage + s->used);
 			if (piece && dma) {
-				hipError_t e = pech_fault(PECH_FAULT_ASYNC_DMA)
-						       ? hipErrorInvalidValue
-						       : hipMemcpyAsync(s->d_stage + s->used, p, piece,
-									hipMemcpyHostToDevice, s->stream);
-				if (e != hipSuccess) {
-					pech_internal_set_err("crc32c_async_submit: payload DMA failed: %s",
-							      hipGetErrorString(e));
-					return fail(fail_cur_slot(a, -EIO));
-				}
+				// issued with the slot's other copies at launch: no HIP
+				// call here (one each cost the caller 5-115 us)
+				s->dma.push_back(DmaCopy{s->d_stage + s->used, const_cast<uint8_t *>(p), piece});
 			} else if (piece) {
 				memcpy(s->h_stage + s->used, p, piece);
 				if (!s->packed.empty() && s->packed.back().second == s->used)

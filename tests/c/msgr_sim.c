@@ -22,7 +22,7 @@
  *
  * Bench mode (bench.py's msgr_async leg):
  *   msgr_sim bench <payload bytes> <count> <mode> <passes>
- * mode 0 async DMA, 1 async zero-copy, 2 messenger adapter, 3 host routine
+ * mode 0 async DMA (CRC32C_ASYNC_DMA), 1 async zero-copy (the default), 2 messenger adapter, 3 host routine
  * (bench_main): <count> payloads of crc32c_pages memory per pass, flushed
  * every 64, completed from an epoll loop; checks every result against the
  * oracle, then prints one JSON line: GiB/s, payloads/s, CPU microseconds per
@@ -196,7 +196,7 @@ static int bench_main(unsigned int size, unsigned int count, unsigned int mode, 
 	if (mode != 3) {
 		struct epoll_event ev;
 
-		a = crc32c_async_create(mode == 0 ? CRC32C_ASYNC_DEFAULT : CRC32C_ASYNC_ZEROCOPY);
+		a = crc32c_async_create(mode == 0 ? CRC32C_ASYNC_DMA : CRC32C_ASYNC_DEFAULT);
 		if (!a)
 			return 2;
 		ep = epoll_create1(0);
@@ -325,7 +325,7 @@ int main(int argc, char **argv)
 		/* the context keeps the device current at creation */
 		if (hipSetDevice((int)(c % (unsigned int)ndev)) != hipSuccess)
 			return 2;
-		ctxs[c] = crc32c_async_create(zerocopy ? CRC32C_ASYNC_ZEROCOPY : CRC32C_ASYNC_DEFAULT);
+		ctxs[c] = crc32c_async_create(zerocopy ? CRC32C_ASYNC_DEFAULT : CRC32C_ASYNC_DMA);
 		if (!ctxs[c]) {
 			fprintf(stderr, "crc32c_async_create: %s\n", crc32c_last_error());
 			return 2;

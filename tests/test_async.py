@@ -55,12 +55,13 @@ def _wait_all(ac, timeout=60.0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("zerocopy", [False, True])
-def test_async_payloads_bit_exact(zerocopy):
+@pytest.mark.parametrize("dma", [False, True])
+def test_async_payloads_bit_exact(dma):
+    # zero-copy (the default) and CRC32C_ASYNC_DMA (copies issued at launch)
     import pech_amd as P
 
-    rng = np.random.default_rng(21 + zerocopy)
-    ac = P.AsyncCrc(zerocopy=zerocopy)
+    rng = np.random.default_rng(21 + dma)
+    ac = P.AsyncCrc(dma=dma)
     sizes = [0, 1, 15, 16, 17, 4095, 4096, 4097, 65536, 1 << 20, (4 << 20) + 5, 123457]
     sizes = sizes * 6 + [int(x) for x in rng.integers(0, 300000, 100)]
     results, expect, keep = {}, {}, []

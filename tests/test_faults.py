@@ -114,33 +114,38 @@ def sc_async_launch_failure_fails_its_slot_then_sticky():
 
 
 def sc_async_dma_failure_mid_slot():
+    # CRC32C_ASYNC_DMA records the payload copies at submit and issues them
+    # when the slot launches: a failed copy fails that slot's payloads
+    # through their callbacks (the submits themselves made no HIP call and
+    # succeeded), makes the error sticky, and drain reports it
     import oracle_lib as O
     import pech_amd as P
 
     rng = np.random.default_rng(43)
-    ac = P.AsyncCrc()  # DMA mode: crc32c_pages payloads are DMA'd to the slot
+    ac = P.AsyncCrc(dma=True)
     pages = [P.Pages(3) for _ in range(4)]
     for pg in pages:
         pg.view[:] = rng.integers(0, 256, pg.nbytes, dtype=np.uint8)
     got = {}
     cb = lambda i: (lambda crc, err: got.__setitem__(i, (crc, err)))  # noqa: E731
     ac.submit(pages[0].ptr, pages[0].nbytes, 0, cb(0))
-    ac.flush()  # payload 0 in flight in its own slot
-    ac.submit(pages[1].ptr, pages[1].nbytes, 1, cb(1))  # slot 2, DMA'd
+    ac.flush()  # payload 0 in flight in its own slot, its copy issued
+    ac.submit(pages[1].ptr, pages[1].nbytes, 1, cb(1))  # slot 2: copies recorded
+    ac.submit(pages[2].ptr, pages[2].nbytes, 2, cb(2))
     inject(SITE_ASYNC_DMA, 1)
-    try:  # payload 2's DMA fails: no callback for it
-        ac.submit(pages[2].ptr, pages[2].nbytes, 2, cb(2))
-        raise AssertionError("submit with a failed DMA returned 0")
-    except P.Crc32cError:
-        pass
-    try:  # drain reports the sticky error after the callbacks ran
+    try:  # the slot's copies fail at its launch
         ac.drain()
         raise AssertionError("drain after a failed slot returned 0")
     except P.Crc32cError:
         pass
     assert got[0] == (O.crc(0, pages[0].view), 0)
-    assert got[1][1] < 0  # shared the failed slot
-    assert 2 not in got and ac.stray == 0
+    assert got[1][1] < 0 and got[2][1] < 0  # the failed slot's payloads
+    try:  # sticky: later submissions are refused, no callback
+        ac.submit(pages[3].ptr, pages[3].nbytes, 3, cb(3))
+        raise AssertionError("submit on a failed context returned 0")
+    except P.Crc32cError:
+        pass
+    assert 3 not in got and ac.stray == 0
     assert ac.pending() == 0
     ac.close()
     for pg in pages:
