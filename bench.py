@@ -342,12 +342,18 @@ def main():
         # Python loop not to be the bound
         if len(set(sizes.tolist())) == 1:
             line["msgr_async"] = msgr_c_bench(args, int(sizes[0]), n)
-            try:  # an auxiliary leg: its failure is reported in the line, not fatal to it
+            try:  # auxiliary legs: a failure is reported in the line, not fatal to it
                 line["msgr_cpu"] = msgr_cpu_sizes(args)
             except (SystemExit, Exception) as e:  # noqa: BLE001
                 line["msgr_cpu"] = {"error": str(e)[:500]}
+            try:
+                line["msgr_latency"] = msgr_latency(args)
+            except (SystemExit, Exception) as e:  # noqa: BLE001
+                line["msgr_latency"] = {"error": str(e)[:500]}
         else:
             line["msgr_async"] = msgr_path(args, bufs[0], offs, sizes, outs, P) if n <= 4096 else None
+    if rank == 0 and world == 1 and len(shards) == 1 and not args.no_host_path and not dsts and args.config == "c3":
+        line["launch_curve"] = launch_curve(shards[0], P, torch)
     if rank == 0 and world == 1 and len(shards) == 1 and not args.no_cpu_baseline and not dsts:
         line["cpu_baseline"] = cpu_baseline(args, bufs[0], offs, sizes, outs, rotate, P)
 
@@ -520,7 +526,8 @@ def msgr_path(args, buf0, offs, sizes, outs, P):
             "bytes_per_pass": nbytes, "passes": args.host_passes, "matches_device_path": True}
 
 
-def msgr_c_bench(args, size, count, modes=(("dma", 0), ("zerocopy", 1), ("adapter", 2), ("host", 3))):
+def msgr_c_bench(args, size, count, modes=(("dma", 0), ("zerocopy", 1), ("adapter", 2), ("host", 3)), passes=None,
+                 env=None):
     """The messenger-side rate and CPU cost from C (build/msgr_sim bench):
     `count` payloads of `size` bytes in crc32c_pages memory per pass, flushed
     every 64 and completed from an epoll loop, through the async layer (DMA
@@ -535,8 +542,8 @@ def msgr_c_bench(args, size, count, modes=(("dma", 0), ("zerocopy", 1), ("adapte
     count = max(1, min(count, (256 << 20) // max(size, 1)))
     res = {}
     for mode, m in modes:
-        r = subprocess.run([exe, "bench", str(size), str(count), str(m), str(args.host_passes)],
-                           capture_output=True, text=True, timeout=300)
+        r = subprocess.run([exe, "bench", str(size), str(count), str(m), str(passes or args.host_passes)],
+                           capture_output=True, text=True, timeout=300, env=dict(os.environ, **(env or {})))
         if r.returncode != 0:
             raise SystemExit(f"msgr_sim bench failed ({r.returncode}): {r.stdout} {r.stderr}")
         d = json.loads(r.stdout.strip().splitlines()[-1])
@@ -570,6 +577,81 @@ def msgr_cpu_sizes(args):
     return {"unit": "CPU us per payload", "sizes": out,
             "path": "build/msgr_sim bench: crc32c_pages payloads, flush every 64, epoll loop; adapter = "
                     "crc32c_msgr_rx_queue/rx_next, host = drop-in crc32c()"}
+
+
+def msgr_latency(args):
+    """Unloaded submit -> verified latency of ONE payload in flight (pech at
+    low queue depth: one read_partial_msg_data -> footer compare per message,
+    messenger.c:2649-2684, :2836-2842), against checksumming it on the host.
+    build/msgr_sim bench with one payload per pass: rx_queue (or the drop-in
+    for "host"), flush, epoll_wait on the eventfd, complete, rx_next.
+    adapter = its default routing (host routine up to 8 KiB); adapter_gpu =
+    PECH_CRC32C_MSGR_HOST_MAX=0, every payload through the GPU (zero-copy
+    read of the pinned page, the direct or plan + main kernels, D2H of the
+    result, host function, eventfd)."""
+    out = {}
+    for size in (4096, 65536, 1 << 20, 4 << 20):
+        r = msgr_c_bench(args, size, 1, modes=(("adapter", 2), ("host", 3)), passes=300)
+        g = msgr_c_bench(args, size, 1, modes=(("adapter_gpu", 2),), passes=300,
+                         env={"PECH_CRC32C_MSGR_HOST_MAX": "0"})
+        out[str(size)] = {k: [v["latency_us_p50"], v["latency_us_p99"], v["thread_cpu_us_per_payload"]]
+                          for k, v in (("adapter", r["adapter"]), ("adapter_gpu", g["adapter_gpu"]),
+                                       ("host", r["host"]))}
+    return {"columns": "[latency p50 us, latency p99 us, calling-thread CPU us] per payload", "sizes": out,
+            "path": "one payload in flight (300 in sequence): crc32c_pages payload, rx_queue, flush, epoll_wait "
+                    "on the eventfd, complete, rx_next; host = drop-in crc32c() on the same bytes"}
+
+
+def launch_curve(shard, P, torch):
+    """Per-launch cost of the planned path (plan + main kernels) against
+    launch size, for 4 MiB and 64 KiB buffers: 4 / 32 (the async layer's
+    slot) / 128 / 256 / 1024 MiB per launch, carved from the shard's resident
+    batches and cycled over distinct regions of them (2 GiB in all, so the
+    256 MB Infinity Cache cannot serve a launch).  main_us: HIP events around
+    each main kernel (its roofline fraction beside it); step_us: wall time
+    per launch of back-to-back serial steps (plan kernel and launch gaps
+    included)."""
+    pool = shard.bufs
+    per = int(pool[0].numel())
+    stream = shard.streams[0]
+    res = {}
+    for bsz in (4 << 20, 64 << 10):
+        row = {}
+        for mib in (4, 32, 128, 256, 1024):
+            tot = mib << 20
+            n = tot // bsz
+            regions = min(512, (per * len(pool)) // tot)
+            descs = []
+            for r in range(regions):
+                b = pool[(r * tot) // per]
+                base = b.data_ptr() + (r * tot) % per
+                descs.append(P.make_descs(base + np.arange(n, dtype=np.int64) * bsz, np.full(n, bsz, np.int64),
+                                          device=shard.dev))
+            out = torch.zeros(n, dtype=torch.int32, device=shard.dev)
+            ws = torch.empty(P.workspace_bytes(n), dtype=torch.uint8, device=shard.dev)
+            k = max(regions, 20)
+            with torch.cuda.device(shard.dev):
+                for i in range(min(k, 8)):  # warm-up
+                    P.dev_batch_ws_async(descs[i % regions], out, ws, stream=stream)
+                torch.cuda.synchronize(shard.dev)
+                P.timing(True)
+                P.timing_read()
+                for i in range(k):
+                    P.dev_batch_ws_async(descs[i % regions], out, ws, stream=stream)
+                torch.cuda.synchronize(shard.dev)
+                P.timing_read()
+                main_us = float(np.mean(np.asarray(P.timing_samples(), dtype=np.float64))) * 1e3
+                P.timing(False)
+                t0 = time.perf_counter()
+                for i in range(k):
+                    P.dev_batch_ws_async(descs[i % regions], out, ws, stream=stream)
+                torch.cuda.synchronize(shard.dev)
+                step_us = (time.perf_counter() - t0) / k * 1e6
+            row[str(mib)] = {"main_us": round(main_us, 2), "frac": round(tot / main_us / 1e3 / HBM_PEAK_GBS, 4),
+                             "step_us": round(step_us, 2), "launches": k}
+        res["4MiB" if bsz == 4 << 20 else "64KiB"] = row
+    return {"unit": "us per launch; frac = launch bytes / main_us / 8 TB/s", "by_buffer_size_then_MiB": res,
+            "path": "crc32c_dev_batch_ws_async (plan + main), one stream"}
 
 
 def sustain(shards, nstreams, seconds, sync_all, dist, backend, dev, torch):

@@ -120,6 +120,10 @@ static struct {
 	int srv_dispatched, srv_dups, cli_dispatched, cli_dups;
 	int srv_faults, cli_faults, cli_resent, pings;
 	int bad_bytes, bad_footer, bad_order, bad_front;
+	long revoke_polls, revoke_out_seen; /* revoke: polls of con->out_msg, distinct messages seen in it */
+	struct ceph_msg *revoke_target;     /* revoke: the message to revoke mid-send */
+	int revoke_queued, revoked_held;
+	struct work_struct revoke_work;
 	int ret;
 } S;
 
@@ -411,6 +415,43 @@ static const struct ceph_connection_operations cli_ops = {
 	.free_msg = lb_free_msg,
 };
 
+/* ---- revoke while the footer is held ------------------------------------
+ * The link wraps the patched messenger's call of crc32c_msgr_tx_footer()
+ * (-Wl,--wrap, tests/pech_build.py): when the revoke target's footer is held
+ * for its GPU CRC, a work item is queued that revokes it as soon as the
+ * connection's work function has let go of the mutex -- before the CRC
+ * lands and the connection is kicked (a poll from the test task could miss
+ * that window: the worker runs queued work back to back).  Inline (no GPU)
+ * there is no held footer; the test task's poll of con->out_msg catches the
+ * message between socket writes instead. */
+int __real_crc32c_msgr_tx_footer(struct crc32c_msgr_conn *c, void *msg, uint32_t *crc);
+
+int __wrap_crc32c_msgr_tx_footer(struct crc32c_msgr_conn *c, void *msg, uint32_t *crc)
+{
+	const int ret = __real_crc32c_msgr_tx_footer(c, msg, crc);
+
+	if (ret == 0 && msg && msg == S.revoke_target && !S.revoke_queued) {
+		S.revoke_queued = 1;
+		queue_work(system_wq, &S.revoke_work);
+	}
+	return ret;
+}
+
+static void revoke_workfn(struct work_struct *w)
+{
+	struct lb_req *r;
+	int i;
+
+	for (i = 0; i < S.nreq; i++) {
+		r = &S.req[i];
+		if (r->m == S.revoke_target && S.ccon.out_msg == r->m && !r->revoked && !r->srv_seen) {
+			r->revoked = 1;
+			ceph_msg_revoke(r->m);
+			S.revoked_held = 1;
+		}
+	}
+}
+
 /* ---- the scenario task -------------------------------------------------- */
 static int all_answered(void)
 {
@@ -445,6 +486,7 @@ static int lb_task(void *arg)
 	struct crc32c_msgr_stats st;
 	u16 srv_port, relay_port;
 	int i, ret, corrupt_idx = -1, revoke_idx = -1, revoked_mid = 0;
+	struct ceph_msg *last_out = NULL;
 	unsigned long deadline;
 
 	S.opt = ceph_alloc_options();
@@ -513,13 +555,20 @@ static int lb_task(void *arg)
 		 * since ceph_con_open): taken off out_queue, never sent */
 		S.req[S.nreq - 1].revoked = 1;
 		ceph_msg_revoke(S.req[S.nreq - 1].m);
+		INIT_WORK(&S.revoke_work, revoke_workfn);
+		S.revoke_target = S.req[revoke_idx].m;
 		/* revoke_idx while it is being written (con->out_msg: its data on
 		 * the wire, or its footer held for the GPU CRC): the rest goes out
 		 * as zeros (write_partial_skip), the server faults on it, and the
 		 * client reconnects and resends everything else.  A message that
 		 * could not be caught mid-send is not revoked, and the run fails. */
-		while (!revoked_mid && time_before(jiffies, deadline) && !S.req[revoke_idx].srv_seen &&
-		       !S.req[revoke_idx].replied) {
+		while (!revoked_mid && !S.revoked_held && time_before(jiffies, deadline) &&
+		       !S.req[revoke_idx].srv_seen && !S.req[revoke_idx].replied) {
+			S.revoke_polls++;
+			if (S.ccon.out_msg && S.ccon.out_msg != last_out) {
+				last_out = S.ccon.out_msg;
+				S.revoke_out_seen++;
+			}
 			if (S.ccon.out_msg == S.req[revoke_idx].m) {
 				S.req[revoke_idx].revoked = 1;
 				ceph_msg_revoke(S.req[revoke_idx].m);
@@ -527,6 +576,7 @@ static int lb_task(void *arg)
 			}
 			schedule();
 		}
+		revoked_mid |= S.revoked_held;
 	}
 	while (!all_answered() && time_before(jiffies, deadline))
 		msleep(2);
@@ -568,16 +618,19 @@ static int lb_task(void *arg)
 			ok = ok && (S.nocrc ? gpu_sub == 0 : st.rx_submitted > 0 && st.tx_submitted > 0) &&
 			     (corrupt_idx < 0 || st.rx_bad >= 1);
 		printf("{\"scenario\": \"%s\", \"ok\": %s, \"requests\": %d, \"unanswered\": %d, \"revoked_mid_send\": %d, "
+		       "\"revoked_footer_held\": %d, "
 		       "\"srv_dispatched\": %d, \"srv_dups\": %d, \"cli_dispatched\": %d, \"cli_dups\": %d, "
 		       "\"pings_skipped\": %d, \"srv_faults\": %d, \"cli_faults\": %d, \"cli_resent\": %d, "
+		       "\"revoke_polls\": %ld, \"revoke_out_seen\": %ld, "
 		       "\"relay_conns\": %d, \"relay_flips\": %d, \"bad_bytes\": %d, \"bad_footer\": %d, "
 		       "\"bad_order\": %d, \"bad_front\": %d, \"msgs_alloc\": %ld, \"msgs_freed\": %ld, "
 		       "\"adapter\": {\"rx_submitted\": %llu, \"rx_host\": %llu, \"rx_unchecked\": %llu, "
 		       "\"rx_verified\": %llu, \"rx_bad\": %llu, \"rx_released\": %llu, \"tx_submitted\": %llu, "
 		       "\"tx_host\": %llu, \"tx_held\": %llu, \"tx_released\": %llu}}\n",
-		       S.scenario, ok ? "true" : "false", S.nreq, unanswered, revoked_mid, S.srv_dispatched, S.srv_dups,
+		       S.scenario, ok ? "true" : "false", S.nreq, unanswered, revoked_mid, S.revoked_held, S.srv_dispatched,
+		       S.srv_dups,
 		       S.cli_dispatched, S.cli_dups, S.pings, S.srv_faults, S.cli_faults, S.cli_resent,
-		       lb_proxy_conns(), lb_proxy_flips(), S.bad_bytes, S.bad_footer, S.bad_order, S.bad_front,
+		       S.revoke_polls, S.revoke_out_seen, lb_proxy_conns(), lb_proxy_flips(), S.bad_bytes, S.bad_footer, S.bad_order, S.bad_front,
 		       S.msgs_alloc, S.msgs_freed, (unsigned long long)st.rx_submitted,
 		       (unsigned long long)st.rx_host, (unsigned long long)st.rx_unchecked,
 		       (unsigned long long)st.rx_verified, (unsigned long long)st.rx_bad,

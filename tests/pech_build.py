@@ -120,7 +120,9 @@ def build_loopback(out):
                 raise RuntimeError(r.stderr[-3000:])
         os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
         tmp = out + ".tmp"
-        r = subprocess.run(["gcc", "-o", tmp, lb, px, orc, *objs, *LINK_LIBS, "-Wl,-rpath,$ORIGIN/../pech_amd"],
+        # the test wraps the messenger's held-footer call (revoke scenario)
+        r = subprocess.run(["gcc", "-o", tmp, lb, px, orc, *objs, *LINK_LIBS, "-Wl,-rpath,$ORIGIN/../pech_amd",
+                            "-Wl,--wrap=crc32c_msgr_tx_footer"],
                            capture_output=True, text=True, timeout=300)
         if r.returncode:
             raise RuntimeError(r.stderr[-3000:])

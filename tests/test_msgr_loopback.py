@@ -33,7 +33,7 @@ def run(scenario, *args, env=None, timeout=150):
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert lines, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     res = json.loads(lines[-1])
-    assert r.returncode == 0 and res["ok"], (res, r.stderr[-3000:])
+    assert r.returncode == 0 and res["ok"], json.dumps(res) + "\n" + r.stderr[-3000:]
     return res
 
 
@@ -44,7 +44,7 @@ def common(res):
     if res["scenario"] in ("corrupt-req", "corrupt-reply"):
         assert res["relay_flips"] == 1 and res["relay_conns"] >= 2 and res["cli_faults"] >= 1
     if res["scenario"] == "revoke":
-        assert res["revoked_mid_send"] == 1 and res["srv_dispatched"] == res["requests"] - 2
+        assert res["revoked_mid_send"] == 1 and res["srv_dispatched"] - res["srv_dups"] == res["requests"] - 2
     if res["scenario"] in ("basic", "nocrc"):
         assert res["srv_dups"] == 0 and res["cli_dups"] == 0 and res["cli_faults"] == 0
         assert res["srv_dispatched"] == res["cli_dispatched"] == res["requests"]
@@ -77,3 +77,5 @@ def test_loopback_gpu(scenario, host_max):
         assert a["rx_submitted"] == a["tx_submitted"] == 0
     if scenario.startswith("corrupt"):
         assert a["rx_bad"] == 1
+    if scenario == "revoke":  # revoked while its footer waited for the GPU CRC
+        assert res["revoked_footer_held"] == 1 and a["tx_released"] >= 1

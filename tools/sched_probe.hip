@@ -18,6 +18,7 @@
 // and a read+write copy probe (same shape, nontemporal loads and stores):
 // the denominator for the fused CRC + copy kernel.
 // Build: make build/sched_probe.  Output: one JSON object.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -1074,6 +1075,56 @@ static const char *sep(void)
 	return g_entries++ ? ",\n" : "";
 }
 
+// launch-cost probe: an empty kernel of the CRC kernel's launch
+// shape, the same with its LDS footprint, the LDS table fill alone (27 KiB of
+// constants -> 128 KiB of bank-replicated tables, one barrier), and a fill
+// followed by the static read of `R` rows
+__global__ __launch_bounds__(1024, 1) void k_empty(uint32_t *out)
+{
+	if (threadIdx.x == 1023u && blockIdx.x == 0x7FFFFFFFu)
+		out[0] = 1u;
+}
+
+template <bool READ>
+__global__ __launch_bounds__(1024, 1) void k_fill(const uint32_t *tab, const uint8_t *p, uint32_t R, uint32_t *out)
+{
+	extern __shared__ uint32_t lds[];
+	const uint32_t tid = threadIdx.x;
+	uint32_t t[4];
+#pragma unroll
+	for (int j = 0; j < 4; ++j)
+		t[j] = tab[tid + j * 1024u]; // 16 KiB of it per workgroup, as the kernel's A_128 tables
+#pragma unroll
+	for (int j = 0; j < 4; ++j)
+#pragma unroll
+		for (int c = 0; c < 8; ++c) // 32 bank copies of 4 KiB = 128 KiB
+			lds[((tid + j * 1024u) * 8u + c) & (32768u - 1u)] = t[j] ^ c;
+	__syncthreads();
+	uint32_t acc = lds[(tid * 37u) & 32767u];
+	if (READ) {
+		const uint32_t W = gridDim.x * WAVES;
+		const uint32_t w = uni(blockIdx.x * WAVES + threadIdx.x / 64u);
+		const uint32_t lane = threadIdx.x & 63u, g8 = lane & 7u, grp = lane >> 3;
+		const uint32_t r0 = (uint32_t)((uint64_t)R * w / W), r1 = (uint32_t)((uint64_t)R * (w + 1u) / W);
+		// the wave's share in 8 group slices, D loads in flight
+		const uint32_t n = r1 - r0, q = n >> 3, rm = n & 7u;
+		const uint32_t st = r0 + grp * q + min(grp, rm), nn = q + (grp < rm ? 1u : 0u);
+		u32x4 v = (u32x4)(0u);
+		for (uint32_t r = 0; r < nn; r += D) {
+			u32x4 ring[D];
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				ring[i] = ld(p, st + min(r + i, nn - 1u), g8);
+#pragma unroll
+			for (int i = 0; i < D; ++i)
+				v ^= ring[i];
+		}
+		acc ^= v.x ^ v.y ^ v.z ^ v.w;
+	}
+	if (acc == 0x12345678u)
+		out[tid] = acc;
+}
+
 // usage: sched_probe [reps] [all|read|copy] [MiB per launch, default 1024]
 // (read: the static read stream only)
 int main(int argc, char **argv)
@@ -1463,6 +1514,54 @@ int main(int argc, char **argv)
 				}
 				printf("%s  {\"probe\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}", sep(), names[v], tot / reps * 1e3,
 				       bytes / (tot / reps * 1e-3) / 1e9);
+			}
+	}
+	if (!strcmp(which, "launch")) {
+		// packet-level durations (hipExtLaunchKernelGGL start/stop events, as
+		// the library times its main kernel) against launch size
+		hipEvent_t a0, a1;
+		CHECK(hipEventCreate(&a0));
+		CHECK(hipEventCreate(&a1));
+		uint32_t *tab;
+		CHECK(hipMalloc(&tab, 6912u * 4u));
+		CHECK(hipMemset(tab, 7, 6912u * 4u));
+		const size_t lds = 144u << 10;
+		CHECK(hipFuncSetAttribute((const void *)k_empty, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		CHECK(hipFuncSetAttribute((const void *)k_fill<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		CHECK(hipFuncSetAttribute((const void *)k_fill<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		CHECK(hipFuncSetAttribute((const void *)k_sched<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		const int mibs[] = {0, 4, 32, 128, 256, 1024};
+		const char *names[] = {"empty, no LDS", "empty, 144 KiB LDS", "table fill only", "static read, no LDS",
+				       "static read, 144 KiB LDS", "table fill + static read", "grid read float4"};
+		for (int v = 0; v < 7; ++v)
+			for (int mi = 0; mi < 6; ++mi) {
+				const int mib = mibs[mi];
+				if ((v < 3) != (mib == 0))
+					continue;
+				const size_t sz = (size_t)mib << 20;
+				const uint32_t Rs = (uint32_t)(sz / ROW);
+				const size_t regions = sz ? (2 * bytes) / sz : 1;
+				float tot = 0;
+				for (int r = -2; r < reps; ++r) {
+					const size_t reg = (size_t)(r + 2) % regions;
+					const uint8_t *pp = sz ? buf[(reg * sz) / bytes] + (reg * sz) % bytes : buf[0];
+					switch (v) {
+					case 0: hipExtLaunchKernelGGL(k_empty, dim3(ncu), dim3(1024), 0, 0, a0, a1, 0, out); break;
+					case 1: hipExtLaunchKernelGGL(k_empty, dim3(ncu), dim3(1024), lds, 0, a0, a1, 0, out); break;
+					case 2: hipExtLaunchKernelGGL(k_fill<false>, dim3(ncu), dim3(1024), lds, 0, a0, a1, 0, tab, pp, Rs, out); break;
+					case 3: hipExtLaunchKernelGGL(k_sched<0>, dim3(ncu), dim3(1024), 0, 0, a0, a1, 0, pp, Rs, ctl, 0u, out, nsteal); break;
+					case 4: hipExtLaunchKernelGGL(k_sched<0>, dim3(ncu), dim3(1024), lds, 0, a0, a1, 0, pp, Rs, ctl, 0u, out, nsteal); break;
+					case 5: hipExtLaunchKernelGGL(k_fill<true>, dim3(ncu), dim3(1024), lds, 0, a0, a1, 0, tab, pp, Rs, out); break;
+					default: hipExtLaunchKernelGGL(k_read_grid<true>, dim3((unsigned)(sz / 16 / 256)), dim3(256), 0, 0, a0, a1, 0, pp, (uint64_t)(sz / 16), out); break;
+					}
+					CHECK(hipEventSynchronize(a1));
+					float ms;
+					CHECK(hipEventElapsedTime(&ms, a0, a1));
+					if (r >= 0)
+						tot += ms;
+				}
+				printf("%s  {\"probe\": \"%s\", \"MiB\": %d, \"us\": %.2f, \"GBps\": %.1f}", sep(), names[v], mib,
+				       tot / reps * 1e3, sz ? sz / (tot / reps * 1e-3) / 1e9 : 0.0);
 			}
 	}
 	if (!strcmp(which, "grid")) { // the best shapes measured: one float4 per thread, non-persistent grid, nt
