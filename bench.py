@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--single-thread", action="store_true",
                     help="pech's model: ONE process drives --gpus devices (hipSetDevice + crc32c_dev_batch_ws_async "
                          "per device, own streams and workspaces), instead of one process per GPU")
+    ap.add_argument("--curve-only", action="store_true",
+                    help="diagnostic (A/B of kernel builds): print only the launch-size curve (launch_curve) of "
+                         "the c3 batches and exit")
     ap.add_argument("--devices", default=None,
                     help="with --single-thread: comma-separated device list (default 0..gpus-1); a repeated id "
                          "puts several shards on one GPU (rehearsal on a 1-GPU box)")
@@ -207,6 +210,9 @@ def main():
 
     shards = [Shard(d, 1000 + rank * 64 + j) for j, d in enumerate(devids)]
     bufs, outs, dsts = shards[0].bufs, shards[0].outs, shards[0].dsts
+    if args.curve_only:
+        print(json.dumps({"kernel": P.version(), "lib": _lib.LIB_PATH, "launch_curve": launch_curve(shards[0], P, torch)}))
+        return
 
     def sync_all():
         for d in sorted(set(devids)):
@@ -363,21 +369,22 @@ def main():
                              "value": round(batch_bytes * steps_done * world * len(shards) / sec / (1 << 30), 2),
                              "unit": "GiB/s"}
     if len(shards) > 1 and dist is None:
-        line["shards_checked"] = shard_parity(shards, offs, sizes, rotate, P)
+        line["shards_checked"], line["buffers_checked"] = shard_parity(shards, offs, sizes, rotate, P)
     if dist is not None:
         # every rank checks its own shard against the oracle (outside the
         # timed region); rank 0 reports how many shards passed
         try:
-            ok = shard_parity(shards, offs, sizes, rotate, P)
+            ok, nbuf = shard_parity(shards, offs, sizes, rotate, P)
             bad = 0
         except SystemExit as e:
             print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
-            ok, bad = 0, 1
-        t = torch.tensor([ok, bad], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+            ok, nbuf, bad = 0, 0, 1
+        t = torch.tensor([ok, bad, nbuf], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         if int(t[1]):
             raise SystemExit(f"PARITY FAILURE: {int(t[1])} rank(s) computed CRCs that differ from the reference")
         line["shards_checked"] = int(t[0])
+        line["buffers_checked"] = int(t[2])
         line["ranks"] = world
     if rank == 0 and world == 1 and len(shards) == 1 and launches:
         probe = stream_probe("copy" if dsts else "read", max(1, batch_bytes >> 20))
@@ -714,24 +721,44 @@ def stream_probe(kind, mib):
 
 
 def shard_parity(shards, offs, sizes, rotate, P):
-    """Multi-shard runs (single-thread, or one rank of a torchrun job): every
-    shard's last outputs for its first and last buffers against the oracle
-    (test infrastructure, outside the timed region)."""
+    """Multi-shard runs (single-thread, or one rank of a torchrun job): EVERY
+    buffer of every shard's rotating batches against the oracle, outside the
+    timed region -- the SSE4.2 batch oracle (oracle/crc32c_hw.c, bit-exact
+    against the compiled reference in tests/test_oracle.py) on 16 host
+    threads, or, on a host without SSE4.2, the reference loop on each batch's
+    first and last buffer.  Returns (shards, buffers) checked."""
     import torch
 
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
 
+    H = O.hw()
+    offs64 = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens32 = np.ascontiguousarray(sizes, dtype=np.uint32)
+    n = len(sizes)
+    checked = 0
     for sh in shards:
         torch.cuda.synchronize(sh.dev)
         for r in range(rotate):
             got = sh.outs[r].cpu().numpy().view(np.uint32)
-            for i in (0, len(sizes) - 1):
-                lo, hi = int(offs[i]), int(offs[i] + sizes[i])
-                want = O.crc(0, sh.bufs[r][lo:hi].cpu().numpy())
-                if int(got[i]) != want:
-                    raise SystemExit(f"PARITY FAILURE: shard on {sh.dev}, batch {r}, buffer {i}")
-    return len(shards)
+            host = sh.bufs[r].cpu().numpy()
+            if H is not None:
+                want = np.zeros(n, dtype=np.uint32)
+                if H.hw_crc32c_batch_mt(host.ctypes.data, offs64.ctypes.data, lens32.ctypes.data, want.ctypes.data,
+                                        n, 16, 1):
+                    raise SystemExit("shard parity: oracle threads failed to start")
+                bad = np.nonzero(got != want)[0]
+                if len(bad):
+                    raise SystemExit(f"PARITY FAILURE: shard on {sh.dev}, batch {r}, {len(bad)} buffer(s), first {bad[0]}")
+                checked += n
+            else:
+                for i in (0, n - 1):
+                    lo, hi = int(offs[i]), int(offs[i] + sizes[i])
+                    if int(got[i]) != O.crc(0, host[lo:hi]):
+                        raise SystemExit(f"PARITY FAILURE: shard on {sh.dev}, batch {r}, buffer {i}")
+                    checked += 1
+            del host
+    return len(shards), checked
 
 
 def cpu_baseline(args, buf0, offs, sizes, outs, rotate, P):

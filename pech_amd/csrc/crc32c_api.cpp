@@ -499,18 +499,20 @@ static int host_big(DevCtx *c, const void *buf, size_t len, uint32_t seed, uint3
 // Descriptors [i0, i0 + m) of one launch: at most STAGE_DESCS, and at most
 // PECH_LAUNCH_MAX_BYTES of payload (the kernels count a launch's rows in
 // 32 bits; only descriptors aliasing the same memory could exceed it).
-static unsigned int launch_take(const unsigned int *lens, unsigned int i0, unsigned int end)
+static unsigned int launch_take(const unsigned int *lens, unsigned int i0, unsigned int end,
+				unsigned int max_descs = STAGE_DESCS)
 {
 	uint64_t bytes = 0;
 	unsigned int m = 0;
-	while (i0 + m < end && m < STAGE_DESCS && (m == 0 || bytes + lens[i0 + m] <= PECH_LAUNCH_MAX_BYTES))
+	while (i0 + m < end && m < max_descs && (m == 0 || bytes + lens[i0 + m] <= PECH_LAUNCH_MAX_BYTES))
 		bytes += lens[i0 + m++];
 	return m;
 }
 
 // CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES: contiguous byte-balanced shards,
-// one per device (PECH_DEVICES="0,0,..." overrides the list; at most two
-// shards per device, on its two slots -- how the 1-GPU tests split a batch).
+// one per device (PECH_DEVICES="0,0,..." overrides the list; up to
+// PECH_MAX_SHARDS_PER_DEV shards per device share its two slots' descriptor
+// space -- how the 1-GPU tests rehearse an 8-GPU split).
 // Every shard's sub-batch is enqueued before any is waited for, so the GPUs
 // read their host links concurrently from this one thread.
 static int shard_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds, uint32_t *out,
@@ -522,6 +524,7 @@ static int shard_pinned(const void *const *bufs, const unsigned int *lens, const
 // segment CRCs are combined on the host, R(s, A || B) = A_|B|(R(s, A)) ^
 // R(0, B), so one huge buffer still keeps every GPU's host link busy.
 #define PECH_SPLIT_MIN_BYTES (16u << 20)
+#define PECH_MAX_SHARDS_PER_DEV 16
 static int multi_device_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
 			       uint32_t *out, unsigned int n)
 {
@@ -545,7 +548,7 @@ static int multi_device_pinned(const void *const *bufs, const unsigned int *lens
 	HIP_TRY(hipGetDeviceCount(&ndev_all));
 	int used[64] = {0};
 	for (int k = 0; k < nd; ++k) {
-		if (devs[k] < 0 || devs[k] >= ndev_all || devs[k] >= 64 || used[devs[k]] >= 2) {
+		if (devs[k] < 0 || devs[k] >= ndev_all || devs[k] >= 64 || used[devs[k]] >= PECH_MAX_SHARDS_PER_DEV) {
 			set_err("crc32c_batch: bad device list (PECH_DEVICES)");
 			return -EINVAL;
 		}
@@ -603,9 +606,20 @@ static int multi_device_pinned(const void *const *bufs, const unsigned int *lens
 static int shard_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds, uint32_t *out,
 			unsigned int n, const int *devs, int nd)
 {
-	int slot[64], used[64] = {0};
+	// shard k: slot slot[k] of its device, descriptors [off[k], off[k] + cap[k])
+	// of it (one shard per device: the whole slot; u shards on one device
+	// split the two slots' STAGE_DESCS between them; a device's shards share
+	// its stream, so they run in order on one workspace)
+	int slot[64], used[64] = {0}, nth[64];
+	unsigned int off[64], cap[64];
 	for (int k = 0; k < nd; ++k)
-		slot[k] = used[devs[k]]++;
+		nth[k] = used[devs[k]]++;
+	for (int k = 0; k < nd; ++k) {
+		const unsigned int per_slot = (unsigned int)(used[devs[k]] + 1) / 2u; // shards sharing one slot
+		slot[k] = nth[k] & 1;
+		cap[k] = STAGE_DESCS / per_slot;
+		off[k] = (unsigned int)(nth[k] >> 1) * cap[k];
+	}
 	// shard k = buffers [cut[k], cut[k+1]): the first buffer whose byte prefix reaches k/nd of the total
 	std::vector<uint64_t> pre(n + 1, 0);
 	for (unsigned int i = 0; i < n; ++i)
@@ -649,30 +663,30 @@ static int shard_pinned(const void *const *bufs, const unsigned int *lens, const
 		more = false;
 		for (int k = 0; k < nd && !rc; ++k) { // enqueue one sub-batch per shard
 			Shard &S = sh[k];
-			S.m = launch_take(lens, S.i0, cut[k + 1]);
+			S.m = launch_take(lens, S.i0, cut[k + 1], cap[k]);
 			if (!S.m)
 				continue;
 			DevCtx *c = S.c;
 			const int s = slot[k];
+			pech_desc *hd = c->h_desc[s] + off[k], *dd = c->d_desc[s] + off[k];
+			uint32_t *ho = c->h_out[s] + off[k], *dout = c->d_out[s] + off[k];
 			if ((rc = hipSetDevice(devs[k]) == hipSuccess ? 0 : -EIO))
 				break;
 			for (unsigned int j = 0; j < S.m; ++j) {
 				const unsigned int i = S.i0 + j;
-				c->h_desc[s][j].addr = dptr[i];
-				c->h_desc[s][j].len = lens[i];
-				c->h_desc[s][j].seed = seeds ? seeds[i] : 0u;
+				hd[j].addr = dptr[i];
+				hd[j].len = lens[i];
+				hd[j].seed = seeds ? seeds[i] : 0u;
 			}
-			if (hipMemcpyAsync(c->d_desc[s], c->h_desc[s], (size_t)S.m * sizeof(pech_desc), hipMemcpyHostToDevice,
-					   c->s_comp) != hipSuccess) {
+			if (hipMemcpyAsync(dd, hd, (size_t)S.m * sizeof(pech_desc), hipMemcpyHostToDevice, c->s_comp) != hipSuccess) {
 				set_err("hipMemcpyAsync: %s", hipGetErrorString(hipGetLastError()));
 				rc = -EIO;
 				break;
 			}
-			// two shards on one device share its stream (ordered), so one workspace serves both
-			if ((rc = launch_batch(c, c->d_desc[s], c->d_out[s], S.m, c->d_ws_host, c->ws_host_bytes, c->s_comp)))
+			// shards on one device share its stream (ordered), so one workspace serves them
+			if ((rc = launch_batch(c, dd, dout, S.m, c->d_ws_host, c->ws_host_bytes, c->s_comp)))
 				break;
-			if (hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t)S.m * 4u, hipMemcpyDeviceToHost, c->s_comp) !=
-			    hipSuccess) {
+			if (hipMemcpyAsync(ho, dout, (size_t)S.m * 4u, hipMemcpyDeviceToHost, c->s_comp) != hipSuccess) {
 				set_err("hipMemcpyAsync: %s", hipGetErrorString(hipGetLastError()));
 				rc = -EIO;
 				break;
@@ -687,7 +701,7 @@ static int shard_pinned(const void *const *bufs, const unsigned int *lens, const
 				rc = -EIO;
 				break;
 			}
-			memcpy(out + S.i0, S.c->h_out[slot[k]], (size_t)S.m * 4u);
+			memcpy(out + S.i0, S.c->h_out[slot[k]] + off[k], (size_t)S.m * 4u);
 			S.i0 += S.m;
 			more = more || S.i0 < cut[k + 1];
 		}

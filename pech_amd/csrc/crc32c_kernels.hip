@@ -456,7 +456,7 @@ extern "C" __global__ __launch_bounds__(PECH_SMALL_THREADS) void pech_crc32c_sma
 // ---- main kernel ----------------------------------------------------------
 #ifdef PECH_STAMPS // diagnostic build: per-wave entry/start/end s_memrealtime stamps
 #define PECH_MAX_STAMPS 8192u
-#define PECH_NSTAMP 12u // start, end, tag, entry, scan, find, plan, fill, 25/50/75% of the first step, spare
+#define PECH_NSTAMP 12u // start, end, tag, entry, scan, find, plan, fill, 25/50/75% of the first step, loads issued
 __device__ uint64_t pech_stamps[PECH_NSTAMP * PECH_MAX_STAMPS];
 #define STAMP(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
 extern "C" int pech_read_stamps(uint64_t *host, uint32_t n)
@@ -847,6 +847,13 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 #define STEP_RA(S) ((uint64_t)((S).mp >> 7) | (uint64_t)((S).oz & PECH_OZ_RA25) >> 4) // rows after the run
 #define STEP_M(S) ((int64_t)(STEP_RA(S) * PECH_ROW_BYTES + ((S).mp & 15u)) - (int64_t)((S).mp & 0x70u))
 
+// a / b with a 32-bit quotient: one 32-bit division when a fits 32 bits
+// (wave-uniform: a scalar branch), the 64-bit sequence otherwise
+__device__ __forceinline__ uint64_t div_u64_u32(uint64_t a, uint32_t b)
+{
+	return (a >> 32) == 0u ? (uint64_t)((uint32_t)a / b) : a / b;
+}
+
 // Ring discipline: row k of a step lives in ring slot k % PECH_U and the
 // lookahead is PECH_U-1 rows.  The iteration that consumes row k first issues
 // the load of row k+PECH_U-1 into the slot row k-1 has just vacated, so no
@@ -998,17 +1005,23 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	constexpr uint32_t TPT = (NT4 + PECH_MAIN_THREADS - 1u) / PECH_MAIN_THREADS;
 	const u32x4 *c4 = (const u32x4 *)(consts + PECH_C_TAB4);
 	uint32_t t128[T128], t16k[T128];
-#pragma unroll
-	for (uint32_t j = 0; j < T128; ++j) {
-		t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
-		t16k[j] = COPY || PECH_IL_CRC ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS] : 0u; // interleaved mode's table
-	}
 	u32x4 tv[TPT];
-#pragma unroll
-	for (uint32_t k = 0; k < TPT; ++k)
-		tv[k] = c4[min(tid + k * PECH_MAIN_THREADS, NT4 - 1u)];
+	uint32_t txi;
 	static_assert(PECH_MAIN_THREADS >= 128u, "inverse powers: one word per thread");
-	const uint32_t txi = consts[PECH_C_XINV + (tid & 127u)];
+	auto load_consts = [&]() {
+#pragma unroll
+		for (uint32_t j = 0; j < T128; ++j) {
+			t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
+			t16k[j] = COPY || PECH_IL_CRC ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS] : 0u; // interleaved mode's table
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < TPT; ++k)
+			tv[k] = c4[min(tid + k * PECH_MAIN_THREADS, NT4 - 1u)];
+		txi = consts[PECH_C_XINV + (tid & 127u)];
+	};
+#ifndef PECH_CONSTS_LAST
+	load_consts();
+#endif
 	// (partials / nzs hold PECH_MAX_CHUNKS entries, lrs whole chunks)
 	u32x4 pv4[4], nv4[4], lr4[4];
 #pragma unroll
@@ -1039,12 +1052,18 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// check below waits for the loads above only).  Unconditional -- a load
 	// under a branch gets a vmcnt(0) at the join -- with lanes past the
 	// chunk's buffers reading lane 0's lines (no extra traffic; masked later).
+#ifndef PECH_LR4_LAZY
 	{
 		const uint32_t ll = lane * 16u < n - cg * PECH_CHUNK ? lane : 0u;
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k)
 			lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + ll * 16u))[k];
 	}
+#endif
+#ifdef PECH_CONSTS_LAST // A/B: the tables' loads after the ones the scan and the start search wait for
+	load_consts();
+#endif
+	STAMP(t_issued);
 
 	// the wave's own exclusive scan of the chunk totals
 	uint32_t pc[16], nc[16], lsum = 0;
@@ -1083,15 +1102,24 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// of rpw_min rows, the last workgroups idle.
 	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_min;
 	const uint32_t rpw = prop ? 0u : rpw_min;
+#ifdef PECH_FAST_DIV // A/B: 32-bit quotients when the products fit 32 bits (batches below 4 GiB / grid rows)
+	const uint64_t wg0 = prop ? div_u64_u32((uint64_t)blockIdx.x * Rtot, gridDim.x)
+				  : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+	const uint32_t wg_rows = prop ? (uint32_t)(div_u64_u32((uint64_t)(blockIdx.x + 1u) * Rtot, gridDim.x) - wg0)
+				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+#else
 	const uint64_t wg0 = prop ? (uint64_t)blockIdx.x * Rtot / gridDim.x : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+#endif
 	if (wg0 >= Rtot)
 		return; // whole workgroup idle (small batch)
 	u32x4 ring[U];
 	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
 	// equal contiguous pieces (age-weighted shares measured no better,
 	// profiles/r01/ab_v5.txt).
+#ifndef PECH_FAST_DIV
 	const uint32_t wg_rows = prop ? (uint32_t)((uint64_t)(blockIdx.x + 1u) * Rtot / gridDim.x - wg0)
 				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+#endif
 	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
 	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
 	// Uniform batches: a wave starts on its share's head [r0, t) and then
@@ -1176,7 +1204,11 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		pjj = pj;
 		nzjj = nzj;
 		const uint32_t rr = r0 - pj;
+#ifdef PECH_LR4_LAZY // A/B: no speculative row offsets (a whole 4 KiB per wave through the TA at entry)
+		if (lane * 16u < nzj) {
+#else
 		if (j != cg && lane * 16u < nzj) { // speculation missed: the start chunk's row offsets now
+#endif
 #pragma unroll
 			for (uint32_t k = 0; k < 4; ++k)
 				lr4[k] = ((const u32x4 *)(lrs + j * PECH_CHUNK + lane * 16u))[k];
@@ -1468,6 +1500,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		st[5] = t_find;
 		st[6] = t_plan;
 		st[7] = t_fill;
+		st[11] = t_issued;
 		st[8] = tq[0];
 		st[9] = tq[1];
 		st[10] = tq[2];

@@ -26,7 +26,9 @@ def test_single_thread_matches_process_per_gpu_schema():
     b = run("--single-thread", "--gpus", "1")
     c = run("--single-thread", "--devices", "0,0")
     assert set(a) == set(b) and set(a["roofline"]) == set(b["roofline"])
-    assert set(c) - set(a) == {"shards_checked"} and c["shards_checked"] == 2
+    assert set(c) - set(a) == {"shards_checked", "buffers_checked"} and c["shards_checked"] == 2
+    # every buffer of both shards' rotating batches checked
+    assert c["buffers_checked"] == 2 * c["config"]["buffers_per_gpu"] * 2
     assert a["n_gpus"] == b["n_gpus"] == c["n_gpus"] == 1
     assert "single-thread" in b["config"]["parallelism"] and "single-thread" in c["config"]["parallelism"]
     # same work on one GPU: the two drivers agree (the bench log records ~1-2 %)
@@ -51,8 +53,8 @@ def test_torchrun_two_ranks_real_kernels():
     d = json.loads(lines[0])
     # n_gpus counts distinct devices: both ranks are on GPU 0
     assert d["n_gpus"] == 1 and d["ranks"] == 2 and d["scaling"] == "weak" and d["value"] > 0
-    # each rank checked its own shard against the oracle
-    assert d["shards_checked"] == 2
+    # each rank checked every buffer of its own shard against the oracle
+    assert d["shards_checked"] == 2 and d["buffers_checked"] == 2 * d["config"]["buffers_per_gpu"] * 2
     assert d["config"]["parallelism"].startswith("shard2")
     assert "cpu_baseline" not in d  # rank 0 at N=1 only
 
@@ -73,3 +75,14 @@ def test_torchrun_rccl_process_group_one_rank():
     assert len(lines) == 1, lines
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["ranks"] == 1 and d["shards_checked"] == 1 and d["value"] > 0
+    assert d["buffers_checked"] == d["config"]["buffers_per_gpu"] * 2
+
+
+def test_single_thread_eight_shards_on_one_gpu():
+    """The 1-GPU rehearsal of pech's one thread driving 8 GPUs (VERDICT r3
+    #4): --single-thread with 8 shards on device 0, every buffer of every
+    shard checked against the oracle."""
+    d = run("--single-thread", "--devices", ",".join(["0"] * 8))
+    assert d["shards_checked"] == 8 and d["n_gpus"] == 1
+    assert d["buffers_checked"] == 8 * d["config"]["buffers_per_gpu"] * 2
+    assert d["value"] > 0

@@ -365,7 +365,7 @@ def test_batch_host_pinned_device_flags(torch_dev, P):
     assert L.crc32c_batch(ptrs, cl, cs, out, n, 3) < 0
 
 
-@pytest.mark.parametrize("devices", [None, "0,0"])
+@pytest.mark.parametrize("devices", [None, "0,0", ",".join(["0"] * 8)])
 def test_batch_pinned_all_devices(torch_dev, P, monkeypatch, devices):
     # CRC32C_F_PINNED | CRC32C_F_ALL_DEVICES: byte-balanced shards, one per GPU,
     # all issued before any wait.  "0,0" = two shards on GPU 0 (both slots,
@@ -399,12 +399,13 @@ def test_batch_pinned_all_devices(torch_dev, P, monkeypatch, devices):
     assert L.crc32c_batch(p1, l1, None, out, 1, P.F_PINNED | P.F_ALL_DEVICES) == -22
 
 
-@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0", ",".join(["0"] * 8), ",".join(["0"] * 17)])
 def test_batch_pinned_all_devices_splits_huge_buffer(torch_dev, P, monkeypatch, devices):
     """A buffer larger than one device's share (>= 16 MiB) is cut into
     per-device segments whose CRCs combine on the host (SURVEY 8e's optional
-    split).  Three "devices" on one GPU: two slots per device at most, so
-    "0,0,0" must be refused; "0,0" splits."""
+    split).  G shards on one GPU rehearse G GPUs (G = 8, the
+    100 MiB buffer cut into 8 page-aligned segments); they share the device's
+    descriptor slots, so more than 16 on one device are refused."""
     torch, dev = torch_dev
     from pech_amd import _lib
 
@@ -423,7 +424,7 @@ def test_batch_pinned_all_devices_splits_huge_buffer(torch_dev, P, monkeypatch, 
     out = (ctypes.c_uint32 * n)()
     L = _lib.lib()
     rc = L.crc32c_batch(ptrs, cl, cs, out, n, P.F_PINNED | P.F_ALL_DEVICES)
-    if devices == "0,0,0":
+    if devices.count(",") + 1 > 16:
         assert rc == -22
         return
     assert rc == 0, L.crc32c_last_error()

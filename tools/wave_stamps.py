@@ -11,6 +11,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 dev = torch.device("cuda:0")
 if cfg == "c3":
     sizes = np.full(256, 4 << 20, dtype=np.int64)
+elif cfg.endswith("x4m"):  # launch-size series: <n> x 4 MiB
+    sizes = np.full(int(cfg[:-3]), 4 << 20, dtype=np.int64)
 elif cfg == "c4":  # bench.py's c4_sizes: equal bytes per class, shuffled with seed 42
     sizes = [4096] * 65536 + [65536] * 4096 + [1 << 20] * 256 + [4 << 20] * 64
     np.random.default_rng(42).shuffle(sizes)
@@ -28,29 +30,37 @@ out = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
 for _ in range(3):
     P.dev_batch_async(descs, out)
 torch.cuda.synchronize()
+P.timing(True)  # the main kernel's packet-level duration (HIP events) for the same launch
+P.timing_read()
+P.dev_batch_async(descs, out)
+torch.cuda.synchronize()
+P.timing_read()
+event_us = float(np.asarray(P.timing_samples())[-1]) * 1e3
+P.timing(False)
 L = _lib.lib()
 L.pech_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 W = 4096
 NS = 12
 st = np.zeros(NS * W, dtype=np.uint64)
 assert L.pech_read_stamps(st.ctypes.data, W) == 0
-s, e, tag, ent, tscan, tfind, tplan, tfill, q1, q2, q3, _ = (st[k::NS].astype(np.int64) for k in range(NS))
+s, e, tag, ent, tscan, tfind, tplan, tfill, q1, q2, q3, tiss = (st[k::NS].astype(np.int64) for k in range(NS))
 ok = (s > 0) & (e > 0)
 s, e, tag, ent = s[ok], e[ok], tag[ok], ent[ok]
-tscan, tfind, tplan, tfill = tscan[ok], tfind[ok], tplan[ok], tfill[ok]
+tscan, tfind, tplan, tfill, tiss = tscan[ok], tfind[ok], tplan[ok], tfill[ok], tiss[ok]
 q1, q2, q3 = q1[ok], q2[ok], q3[ok]
 xcc, blk = tag & 0xF, tag >> 8
 # s_memrealtime: 100 MHz chip-wide clock (10 ns ticks)
 t0 = ent.min()
-s -= t0; e -= t0; ent -= t0; tscan -= t0; tfind -= t0; tplan -= t0; tfill -= t0
+s -= t0; e -= t0; ent -= t0; tscan -= t0; tfind -= t0; tplan -= t0; tfill -= t0; tiss -= t0
 q1 -= t0; q2 -= t0; q3 -= t0
 pro = s - ent
 span = e.max()
 pct = lambda a, q: float(np.percentile(a, q))
-print(f"{cfg}: waves {ok.sum()}, span {span*10/1000:.1f} us")
+print(f"{cfg}: waves {ok.sum()}, span {span*10/1000:.1f} us (entry of the first wave to end of the last); "
+      f"main-kernel event duration {event_us:.1f} us")
 print("entry us p50/p99/max: %.1f %.1f %.1f" % (pct(ent,50)/100, pct(ent,99)/100, ent.max()/100))
 print("prologue (entry->first row) us p10/p50/p90/max: %.1f %.1f %.1f %.1f" % (pct(pro,10)/100, pct(pro,50)/100, pct(pro,90)/100, pro.max()/100))
-for nm, a, b in (("entry->scan", ent, tscan), ("scan->find", tscan, tfind), ("find->plan", tfind, tplan),
+for nm, a, b in (("entry->issued", ent, tiss), ("issued->scan", tiss, tscan), ("scan->find", tscan, tfind), ("find->plan", tfind, tplan),
                  ("plan->fill", tplan, tfill), ("fill->start(barrier)", tfill, s)):
     d = b - a
     print("  %-22s us p10/p50/p90: %.2f %.2f %.2f" % (nm, pct(d, 10) / 100, pct(d, 50) / 100, pct(d, 90) / 100))
