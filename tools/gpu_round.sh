@@ -19,8 +19,10 @@ for cfg in ${STAMP_CONFIGS:-}; do
     || stop $? "stamps $cfg"
   grep -v "amdgpu.ids\|^xcc\|histogram" gpurun_out/stamps_$cfg.txt
 done
-# columns: value (2-stream pass) GiB/s, main GB/s, roofline frac, main us, serial (1-stream) GiB/s
+# columns: value (2-stream pass) GiB/s, main GB/s, roofline frac, main us, serial (1-stream) GiB/s,
+# sustained GiB/s (with AB_EXTRA="--sustain-seconds 4"); AB_EXTRA="--op copy" A/Bs the fused copy
 # AB_ENVS: space-separated variants, each a comma-separated VAR=value list ("-" = none)
+for pass in $(seq 1 ${PASSES:-1}); do
 for ev in ${AB_ENVS:--}; do
 for lib in ${AB_LIBS:-pech_amd/libpech_crc32c.so}; do
   for cfg in ${AB_CONFIGS:-c3}; do
@@ -28,8 +30,9 @@ for lib in ${AB_LIBS:-pech_amd/libpech_crc32c.so}; do
     envs=""; [ "$ev" != - ] && envs=${ev//,/ }
     env $envs PECH_CRC32C_LIB=$lib timeout -k 10 240 python bench.py --config $cfg --steps 30 --no-cpu-baseline --no-host-path \
       ${AB_EXTRA:-} > $o 2>&1 || { tail -5 $o; stop $? "bench $lib $cfg"; }
-    echo "$(basename $lib) $ev $cfg: $(tail -1 $o | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["achieved"], r["frac"], r["avg_launch_us"], d.get("serial", {}).get("value"))')"
+    echo "$(basename $lib) $ev $cfg: $(tail -1 $o | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["achieved"], r["frac"], r["avg_launch_us"], d.get("serial", {}).get("value"), d.get("sustained", {}).get("value"))')"
   done
+done
 done
 done
 exit 0
