@@ -237,6 +237,10 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	__shared__ uint32_t scratch[PECH_WAVES_PER_WG];
 	__shared__ uint32_t rmax; // largest core of the chunk (uniformity flag)
 	const uint32_t tid = threadIdx.x;
+#ifdef PECH_KARGS_AT_ENTRY
+	asm volatile("" ::"s"(descs), "s"(n), "s"(cores), "s"(lrs), "s"(partials), "s"(nzs), "s"(consts), "s"(out), "s"(dsts),
+		     "s"(deltas)); // one kernarg round (main_body)
+#endif
 	const uint32_t b = blockIdx.x * PECH_CHUNK + tid;
 	// loads unconditional (clamped indices) so they are in flight together:
 	// loads under exec-masked branches each got a vmcnt(0) at the join
@@ -970,6 +974,241 @@ __device__ __forceinline__ uint32_t share_head(uint32_t a, uint32_t b)
 	return min(b, max(a + PECH_ITEM_ROWS, b - min(PECH_POOL_ROWS, b - a)));
 }
 
+// What a main-kernel wave knows after the chunk scan and the start search
+// (prologue_start): all wave-uniform.
+struct Start {
+	uint32_t U0, wg_rows, r0, r1, jmax, rem_all, p0, lr0, jj, pjj, nzjj, nsjj;
+	uint64_t wg0;
+	bool uniform, il;
+#ifdef PECH_STAMPS
+	uint64_t t_scan;
+#endif
+};
+
+// The main kernel's chunk scan and start search, with CPL chunks per lane
+// (4: batches of up to 256 chunks, 16: up to PECH_MAX_CHUNKS).  Every wave
+// scans the chunk totals itself (no workgroup scan, no barrier), takes its
+// equal share [r0, r1) of the rows, and locates r0: first at the speculated
+// position pg (exact for uniform batches), else by a search over the chunk
+// prefixes and the start chunk's row offsets (lr4, reloaded when the
+// speculated chunk was wrong).  It also writes the chunk non-empty counts to
+// LDS for plan_step.  Returns false when the whole workgroup is idle.
+template <bool COPY, uint32_t CPL>
+__device__ __forceinline__ bool prologue_start(uint32_t *lds, const pech_core *__restrict__ cores,
+					       const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
+					       const uint32_t *__restrict__ nzs, uint32_t n, uint32_t nchunks, uint32_t lane,
+					       uint32_t wave, uint32_t W, uint32_t rpw_min, uint32_t pg, uint32_t cg,
+					       uint32_t lrg, const pech_core &spec, u32x4 (&lr4)[4], Start &st)
+{
+	static_assert(CPL == 4u || CPL == 16u, "chunks per lane");
+	static_assert(64u * 16u == PECH_MAX_CHUNKS, "16 chunks per lane cover every chunk");
+	// (partials / nzs hold PECH_MAX_CHUNKS entries in the workspace: CPL = 4
+	// reads the first 256 of each unconditionally, entries past nchunks are
+	// masked)
+	u32x4 pv4[CPL / 4u], nv4[CPL / 4u];
+	if (CPL == 4u) {
+		pv4[0] = ((const u32x4 *)partials)[lane];
+		nv4[0] = ((const u32x4 *)nzs)[lane];
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < CPL / 4u; ++k) // defined values where nothing loads (a select of undef may fold)
+			pv4[k] = nv4[k] = (u32x4)(0u);
+		if (lane * CPL < nchunks) {
+#pragma unroll
+			for (uint32_t k = 0; k < CPL / 4u; ++k) {
+				pv4[k] = ((const u32x4 *)partials)[lane * (CPL / 4u) + k];
+				nv4[k] = ((const u32x4 *)nzs)[lane * (CPL / 4u) + k];
+			}
+		}
+	}
+	// the wave's own exclusive scan of the chunk totals
+	uint32_t pc[CPL], nc[CPL], lsum = 0;
+	bool uflag = true;
+#pragma unroll
+	for (uint32_t k = 0; k < CPL; ++k) {
+		const bool real = lane * CPL + k < nchunks;
+		const uint32_t nzf = real ? nv4[k >> 2][k & 3u] : PECH_NZ_UNIFORM;
+		pc[k] = real ? pv4[k >> 2][k & 3u] : 0u;
+		nc[k] = nzf & ~PECH_NZ_UNIFORM; // non-empty | small cores << PECH_NS_SHIFT
+		uflag = uflag && (nzf & PECH_NZ_UNIFORM) != 0u;
+		lsum += pc[k];
+	}
+	const uint32_t incl = wave_incl_scan(lsum);
+	const uint32_t Rtot = lane_value(incl, 63);
+	// Uniform batch (every chunk flagged by the plan kernel, all with chunk
+	// 0's rows per buffer): position p holds rows [p U0, (p+1) U0), so any row
+	// is located by a division, and the workgroup pools its rows in items.
+	const uint32_t nz0 = lane_value(nc[0], 0) & PECH_NZ_MASK; // (lane values: wave-uniform, as the pool needs)
+	const uint32_t U0 = nz0 ? lane_value(pc[0], 0) / nz0 : 0u;
+	bool uok = uflag;
+#pragma unroll
+	for (uint32_t k = 0; k < CPL; ++k)
+		uok = uok && (uint64_t)(nc[k] & PECH_NZ_MASK) * U0 == (uint64_t)pc[k];
+	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
+	// fused copy of a uniform batch of large buffers: interleaved rows (plan_il)
+	const bool il = (COPY ? PECH_IL_COPY : PECH_IL_CRC) && uniform && U0 >= PECH_IL_MIN_ROWS;
+	STAMP(t_scan);
+#ifdef PECH_STAMPS
+	st.t_scan = t_scan;
+#endif
+	// Every wave gets an equal share of the batch's rows (at least rpw_min).
+	// Large batches: workgroup b gets rows [b Rtot / G, (b+1) Rtot / G) --
+	// proportional, not b * ceil(Rtot / W): the rounding drifted by up to a
+	// row per wave, a whole step of 8 small buffers after a few hundred
+	// waves, so some waves walked an extra step (2 -> 3 on unaligned
+	// 4,100-byte buffers) and set the launch's end.  Small batches: shares
+	// of rpw_min rows, the last workgroups idle.
+	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_min;
+	const uint32_t rpw = prop ? 0u : rpw_min;
+#ifdef PECH_FAST_DIV // A/B: 32-bit quotients when the products fit 32 bits (batches below 4 GiB / grid rows)
+	const uint64_t wg0 = prop ? div_u64_u32((uint64_t)blockIdx.x * Rtot, gridDim.x)
+				  : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+	const uint32_t wg_rows = prop ? (uint32_t)(div_u64_u32((uint64_t)(blockIdx.x + 1u) * Rtot, gridDim.x) - wg0)
+				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+#else
+	const uint64_t wg0 = prop ? (uint64_t)blockIdx.x * Rtot / gridDim.x : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+#endif
+	if (wg0 >= Rtot)
+		return false; // whole workgroup idle (small batch)
+	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
+	// equal contiguous pieces (age-weighted shares measured no better,
+	// profiles/r01/ab_v5.txt).
+#ifndef PECH_FAST_DIV
+	const uint32_t wg_rows = prop ? (uint32_t)((uint64_t)(blockIdx.x + 1u) * Rtot / gridDim.x - wg0)
+				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+#endif
+	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
+	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
+	// Uniform batches: a wave starts on its share's head [r0, t) and then
+	// takes items of PECH_ITEM_ROWS rows from the workgroup's pool of share
+	// tails (at most PECH_POOL_ROWS of each share; an LDS counter, claim c is
+	// tail item c/16 of share c%16, located by division), so the CU's 16
+	// waves -- issued oldest-first, which made equal static shares finish up
+	// to 60 us apart -- end together, and the CU is free for the next
+	// launch's workgroup that much earlier.  (The fused copy keeps static
+	// shares: pooled items cost it 9-14 % per launch, profiles/r02/ab_item_pool.txt.)
+	// Shares below PECH_POOL_MIN_SHARE rows keep static shares too: a 512-row
+	// share (256 MiB of 64 KiB-4 MiB buffers) pooled is a 256-row head and one
+	// item, i.e. runs of 32 rows with a fold each; static, one step of 64-row
+	// runs: 48.8 instead of 51.5-53.4 us per launch (profiles/r03/ab_pool_min_share.txt).
+#ifdef PECH_NO_POOL // A/B: static shares for every batch
+	const uint32_t jmax = 0u;
+#else
+	const uint32_t jmax = !COPY && !il && uniform && wg_rows >= PECH_MAIN_WAVES * PECH_POOL_MIN_SHARE
+				      ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
+										      PECH_MAIN_WAVES) + PECH_ITEM_ROWS - 1u) /
+							     PECH_ITEM_ROWS
+					       : 0u;
+#endif
+	uint32_t rem_all = jmax ? share_head(r0, r1) - r0 : r1 - r0;
+	// nz table for plan_step: every wave writes all of it (the same values)
+	// and reads back only its own writes until the barrier below
+#pragma unroll
+	for (uint32_t k = 0; k < CPL / 4u; ++k)
+		*(u32x4 *)(lds + L_NZ / 4u + lane * CPL + 4u * k) =
+			u32x4{nc[4 * k], nc[4 * k + 1], nc[4 * k + 2], nc[4 * k + 3]} & PECH_NZ_MASK; // braces: a parenthesised list is a comma splat
+
+	uint32_t p0 = 0, lr0 = 0;
+	bool found = false;
+	// the start chunk's prefix, non-empty and small cores, and rows (grid snap below)
+	uint32_t jj = 0, pjj = 0, nzjj = 0, nsjj = 0;
+	if (rem_all) {
+		// The speculated position first, checked exactly: buffer pg holds
+		// row r0 iff its global offset (chunk prefix + lrs[pg]) <= r0 <
+		// offset + its rows.  Uniform batches start here without waiting for
+		// the row-offset scan below.
+		const uint32_t lc = cg / CPL, kc = cg % CPL;
+		uint32_t prec = incl - lsum, nzc = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < CPL; ++k) {
+			prec += k < kc ? pc[k] : 0u;
+			nzc = k == kc ? nc[k] : nzc;
+		}
+		const uint32_t og = lane_value(prec, lc) + uni(lrg);
+		const uint32_t rg = uni(spec.rows); // lane 0: cores[pg]
+		if (cg < nchunks && (pg & 1023u) < (lane_value(nzc, lc) & PECH_NZ_MASK) && og <= r0 && r0 - og < rg) {
+			p0 = pg;
+			lr0 = r0 - og;
+			found = true;
+			jj = cg;
+			pjj = lane_value(prec, lc);
+			nzjj = lane_value(nzc, lc);
+			nsjj = nzjj >> PECH_NS_SHIFT;
+			nzjj &= PECH_NZ_MASK;
+		}
+	}
+	if (rem_all && !found) {
+		// start chunk j: the last chunk whose prefix is <= r0 (non-empty,
+		// since r0 < Rtot); its prefix and non-empty count
+		uint32_t pre = incl - lsum, cnt = 0, pj = 0, nzj = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < CPL; ++k) {
+			const bool le = lane * CPL + k < nchunks && pre <= r0;
+			cnt += le ? 1u : 0u;
+			pj = le ? pre : pj;
+			nzj = le ? nc[k] : nzj;
+			pre += pc[k];
+		}
+		// (prefixes are nondecreasing: the lanes with cnt > 0 are a prefix)
+		const uint32_t Lj = last_lane_with(cnt);
+		const uint32_t j = Lj * CPL + lane_value(cnt, Lj) - 1u;
+		pj = lane_value(pj, Lj);
+		nzj = lane_value(nzj, Lj);
+		nsjj = nzj >> PECH_NS_SHIFT;
+		nzj &= PECH_NZ_MASK;
+		jj = j;
+		pjj = pj;
+		nzjj = nzj;
+		const uint32_t rr = r0 - pj;
+#ifdef PECH_LR4_LAZY // A/B: no speculative row offsets (a whole 4 KiB per wave through the TA at entry)
+		if (lane * 16u < nzj) {
+#else
+		if (j != cg && lane * 16u < nzj) { // speculation missed: the start chunk's row offsets now
+#endif
+#pragma unroll
+			for (uint32_t k = 0; k < 4; ++k)
+				lr4[k] = ((const u32x4 *)(lrs + j * PECH_CHUNK + lane * 16u))[k];
+		}
+		// position: the count of the chunk's offsets <= rr (nondecreasing
+		// over its nz non-empty cores), and the row inside that buffer
+		uint32_t c2 = 0, lo = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 16; ++k) {
+			const uint32_t e = lr4[k >> 2][k & 3u];
+			const bool ok = lane * 16u + k < nzj && e <= rr;
+			c2 += ok ? 1u : 0u;
+			lo = ok ? max(lo, e) : lo;
+		}
+		// (offsets increase over the non-empty cores: the lanes with c2 > 0
+		// are a prefix, and the last of them holds the largest offset <= rr)
+		const uint32_t Lp = last_lane_with(c2);
+		const uint32_t cpos = Lp * 16u + lane_value(c2, Lp);
+		p0 = j * PECH_CHUNK + cpos - 1u;
+		lr0 = rr - lane_value(lo, Lp);
+#ifdef PECH_DEBUG_BOUNDS
+		if (lane == 0 && (j >= nchunks || cpos == 0 || cpos > nzj || lr0 >= cores[p0].rows))
+			printf("PECH OOB prologue blk %u wave %u r0 %u j %u cg %u nchunks %u nzj %u cpos %u rr %u rows %u\n",
+			       blockIdx.x, wave, r0, j, cg, nchunks, nzj, cpos, rr, cores[min(p0, nchunks * PECH_CHUNK - 1u)].rows);
+#endif
+	}
+	st.U0 = U0;
+	st.wg_rows = wg_rows;
+	st.r0 = r0;
+	st.r1 = r1;
+	st.jmax = jmax;
+	st.rem_all = rem_all;
+	st.p0 = p0;
+	st.lr0 = lr0;
+	st.jj = jj;
+	st.pjj = pjj;
+	st.nzjj = nzjj;
+	st.nsjj = nsjj;
+	st.wg0 = wg0;
+	st.uniform = uniform;
+	st.il = il;
+	return true;
+}
+
 template <bool COPY, uint32_t U>
 __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
 					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
@@ -979,6 +1218,13 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 {
 	const uint32_t tid = threadIdx.x;
 	STAMP(t_entry);
+#ifdef PECH_KARGS_AT_ENTRY
+	// every kernel argument in SGPRs at entry, in one scalar round: on demand,
+	// LLVM loaded them in three rounds, each gating the next group of the
+	// prologue's vector loads (kernarg reads are scalar-cache misses at entry)
+	asm volatile("" ::"s"(cores), "s"(lrs), "s"(partials), "s"(nzs), "s"(n), "s"(consts), "s"(out), "s"(rpw_min),
+		     "s"(deltas));
+#endif
 	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
 	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
 	const uint32_t wave = uni(tid >> 6);
@@ -1022,18 +1268,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifndef PECH_CONSTS_LAST
 	load_consts();
 #endif
-	// (partials / nzs hold PECH_MAX_CHUNKS entries, lrs whole chunks)
-	u32x4 pv4[4], nv4[4], lr4[4];
-#pragma unroll
-	for (uint32_t k = 0; k < 4; ++k) // defined values where nothing loads (a select of undef may fold)
-		pv4[k] = nv4[k] = lr4[k] = (u32x4)(0u);
-	if (lane * 16u < nchunks) {
-#pragma unroll
-		for (uint32_t k = 0; k < 4; ++k) {
-			pv4[k] = ((const u32x4 *)partials)[lane * 4u + k];
-			nv4[k] = ((const u32x4 *)nzs)[lane * 4u + k];
-		}
-	}
+	// the speculative start (below), its chunk's row offsets, then the chunk totals
+	u32x4 lr4[4];
 	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
 	// likely start position: exact for uniform batches (a double quotient of
 	// integers is exact when it is one; a near miss only costs a reload)
@@ -1048,10 +1284,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		spec.meta = v.w;
 	}
 
-	// last: the speculative row offsets (vmcnt is in order, so the exact
-	// check below waits for the loads above only).  Unconditional -- a load
-	// under a branch gets a vmcnt(0) at the join -- with lanes past the
-	// chunk's buffers reading lane 0's lines (no extra traffic; masked later).
+	// the speculative row offsets.  Unconditional -- a load under a branch
+	// gets a vmcnt(0) at the join -- with lanes past the chunk's buffers
+	// reading lane 0's lines (no extra traffic; masked later).
 #ifndef PECH_LR4_LAZY
 	{
 		const uint32_t ll = lane * 16u < n - cg * PECH_CHUNK ? lane : 0u;
@@ -1059,182 +1294,39 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		for (uint32_t k = 0; k < 4; ++k)
 			lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + ll * 16u))[k];
 	}
+#else
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k)
+		lr4[k] = (u32x4)(0u);
 #endif
 #ifdef PECH_CONSTS_LAST // A/B: the tables' loads after the ones the scan and the start search wait for
 	load_consts();
 #endif
 	STAMP(t_issued);
 
-	// the wave's own exclusive scan of the chunk totals
-	uint32_t pc[16], nc[16], lsum = 0;
-	bool uflag = true;
-#pragma unroll
-	for (uint32_t k = 0; k < 16; ++k) {
-		const bool real = lane * 16u + k < nchunks;
-		const uint32_t nzf = real ? nv4[k >> 2][k & 3u] : PECH_NZ_UNIFORM;
-		pc[k] = real ? pv4[k >> 2][k & 3u] : 0u;
-		nc[k] = nzf & ~PECH_NZ_UNIFORM; // non-empty | small cores << PECH_NS_SHIFT
-		uflag = uflag && (nzf & PECH_NZ_UNIFORM) != 0u;
-		lsum += pc[k];
-	}
-	const uint32_t incl = wave_incl_scan(lsum);
-	const uint32_t Rtot = lane_value(incl, 63);
-	// Uniform batch (every chunk flagged by the plan kernel, all with chunk
-	// 0's rows per buffer): position p holds rows [p U0, (p+1) U0), so any row
-	// is located by a division, and the workgroup pools its rows in items.
-	const uint32_t nz0 = lane_value(nc[0], 0) & PECH_NZ_MASK; // (lane values: wave-uniform, as the pool needs)
-	const uint32_t U0 = nz0 ? lane_value(pc[0], 0) / nz0 : 0u;
-	bool uok = uflag;
-#pragma unroll
-	for (uint32_t k = 0; k < 16; ++k)
-		uok = uok && (uint64_t)(nc[k] & PECH_NZ_MASK) * U0 == (uint64_t)pc[k];
-	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
-	// fused copy of a uniform batch of large buffers: interleaved rows (plan_il)
-	const bool il = (COPY ? PECH_IL_COPY : PECH_IL_CRC) && uniform && U0 >= PECH_IL_MIN_ROWS;
-	const uint32_t rsb = il ? PECH_IL_GROUPS * PECH_ROW_BYTES : PECH_ROW_BYTES; // bytes from one row of a run to the next
-	STAMP(t_scan);
-	// Every wave gets an equal share of the batch's rows (at least rpw_min).
-	// Large batches: workgroup b gets rows [b Rtot / G, (b+1) Rtot / G) --
-	// proportional, not b * ceil(Rtot / W): the rounding drifted by up to a
-	// row per wave, a whole step of 8 small buffers after a few hundred
-	// waves, so some waves walked an extra step (2 -> 3 on unaligned
-	// 4,100-byte buffers) and set the launch's end.  Small batches: shares
-	// of rpw_min rows, the last workgroups idle.
-	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_min;
-	const uint32_t rpw = prop ? 0u : rpw_min;
-#ifdef PECH_FAST_DIV // A/B: 32-bit quotients when the products fit 32 bits (batches below 4 GiB / grid rows)
-	const uint64_t wg0 = prop ? div_u64_u32((uint64_t)blockIdx.x * Rtot, gridDim.x)
-				  : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
-	const uint32_t wg_rows = prop ? (uint32_t)(div_u64_u32((uint64_t)(blockIdx.x + 1u) * Rtot, gridDim.x) - wg0)
-				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
-#else
-	const uint64_t wg0 = prop ? (uint64_t)blockIdx.x * Rtot / gridDim.x : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
-#endif
-	if (wg0 >= Rtot)
+	// The chunk scan and the start search (prologue_start): four chunks per
+	// lane for batches of up to 256 chunks (262,144 buffers), sixteen beyond.
+	// Every wave of the CU runs it, so its instruction count is the prologue's
+	// cost: a wave64 VALU instruction issues every 4 cycles per SIMD and four
+	// waves share a SIMD (the 16-per-lane loops alone were ~1 us of it).
+	Start sv;
+	const bool live = nchunks <= 64u * 4u
+			  ? prologue_start<COPY, 4>(lds, cores, lrs, partials, nzs, n, nchunks, lane, wave, W, rpw_min, pg,
+						    cg, lrg, spec, lr4, sv)
+			  : prologue_start<COPY, 16>(lds, cores, lrs, partials, nzs, n, nchunks, lane, wave, W, rpw_min, pg,
+						     cg, lrg, spec, lr4, sv);
+	if (!live)
 		return; // whole workgroup idle (small batch)
+#ifdef PECH_STAMPS
+	const uint64_t t_scan = sv.t_scan;
+#endif
+	const uint32_t U0 = sv.U0, wg_rows = sv.wg_rows, r0 = sv.r0, r1 = sv.r1, jmax = sv.jmax;
+	const uint64_t wg0 = sv.wg0;
+	const bool il = sv.il;
+	const uint32_t rsb = il ? PECH_IL_GROUPS * PECH_ROW_BYTES : PECH_ROW_BYTES; // bytes from one row of a run to the next
+	uint32_t rem_all = sv.rem_all, p0 = sv.p0, lr0 = sv.lr0;
+	const uint32_t jj = sv.jj, pjj = sv.pjj, nzjj = sv.nzjj, nsjj = sv.nsjj;
 	u32x4 ring[U];
-	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
-	// equal contiguous pieces (age-weighted shares measured no better,
-	// profiles/r01/ab_v5.txt).
-#ifndef PECH_FAST_DIV
-	const uint32_t wg_rows = prop ? (uint32_t)((uint64_t)(blockIdx.x + 1u) * Rtot / gridDim.x - wg0)
-				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
-#endif
-	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
-	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
-	// Uniform batches: a wave starts on its share's head [r0, t) and then
-	// takes items of PECH_ITEM_ROWS rows from the workgroup's pool of share
-	// tails (at most PECH_POOL_ROWS of each share; an LDS counter, claim c is
-	// tail item c/16 of share c%16, located by division), so the CU's 16
-	// waves -- issued oldest-first, which made equal static shares finish up
-	// to 60 us apart -- end together, and the CU is free for the next
-	// launch's workgroup that much earlier.  (The fused copy keeps static
-	// shares: pooled items cost it 9-14 % per launch, profiles/r02/ab_item_pool.txt.)
-	// Shares below PECH_POOL_MIN_SHARE rows keep static shares too: a 512-row
-	// share (256 MiB of 64 KiB-4 MiB buffers) pooled is a 256-row head and one
-	// item, i.e. runs of 32 rows with a fold each; static, one step of 64-row
-	// runs: 48.8 instead of 51.5-53.4 us per launch (profiles/r03/ab_pool_min_share.txt).
-#ifdef PECH_NO_POOL // A/B: static shares for every batch
-	const uint32_t jmax = 0u;
-#else
-	const uint32_t jmax = !COPY && !il && uniform && wg_rows >= PECH_MAIN_WAVES * PECH_POOL_MIN_SHARE
-				      ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
-										      PECH_MAIN_WAVES) + PECH_ITEM_ROWS - 1u) /
-							     PECH_ITEM_ROWS
-					       : 0u;
-#endif
-	uint32_t rem_all = jmax ? share_head(r0, r1) - r0 : r1 - r0;
-
-	// nz table for plan_step: every wave writes all of it (the same values)
-	// and reads back only its own writes until the barrier below
-#pragma unroll
-	for (uint32_t k = 0; k < 4; ++k)
-		*(u32x4 *)(lds + L_NZ / 4u + lane * 16u + 4u * k) =
-			u32x4{nc[4 * k], nc[4 * k + 1], nc[4 * k + 2], nc[4 * k + 3]} & PECH_NZ_MASK; // braces: a parenthesised list is a comma splat
-
-	uint32_t p0 = 0, lr0 = 0;
-	bool found = false;
-	// the start chunk's prefix, non-empty and small cores, and rows (grid snap below)
-	uint32_t jj = 0, pjj = 0, nzjj = 0, nsjj = 0;
-	if (rem_all) {
-		// The speculated position first, checked exactly: buffer pg holds
-		// row r0 iff its global offset (chunk prefix + lrs[pg]) <= r0 <
-		// offset + its rows.  Uniform batches start here without waiting for
-		// the row-offset scan below.
-		const uint32_t lc = cg >> 4, kc = cg & 15u;
-		uint32_t prec = incl - lsum, nzc = 0;
-#pragma unroll
-		for (uint32_t k = 0; k < 16; ++k) {
-			prec += k < kc ? pc[k] : 0u;
-			nzc = k == kc ? nc[k] : nzc;
-		}
-		const uint32_t og = lane_value(prec, lc) + uni(lrg);
-		const uint32_t rg = uni(spec.rows); // lane 0: cores[pg]
-		if (cg < nchunks && (pg & 1023u) < (lane_value(nzc, lc) & PECH_NZ_MASK) && og <= r0 && r0 - og < rg) {
-			p0 = pg;
-			lr0 = r0 - og;
-			found = true;
-			jj = cg;
-			pjj = lane_value(prec, lc);
-			nzjj = lane_value(nzc, lc);
-			nsjj = nzjj >> PECH_NS_SHIFT;
-			nzjj &= PECH_NZ_MASK;
-		}
-	}
-	if (rem_all && !found) {
-		// start chunk j: the last chunk whose prefix is <= r0 (non-empty,
-		// since r0 < Rtot); its prefix and non-empty count
-		uint32_t pre = incl - lsum, cnt = 0, pj = 0, nzj = 0;
-#pragma unroll
-		for (uint32_t k = 0; k < 16; ++k) {
-			const bool le = lane * 16u + k < nchunks && pre <= r0;
-			cnt += le ? 1u : 0u;
-			pj = le ? pre : pj;
-			nzj = le ? nc[k] : nzj;
-			pre += pc[k];
-		}
-		// (prefixes are nondecreasing: the lanes with cnt > 0 are a prefix)
-		const uint32_t Lj = last_lane_with(cnt);
-		const uint32_t j = Lj * 16u + lane_value(cnt, Lj) - 1u;
-		pj = lane_value(pj, Lj);
-		nzj = lane_value(nzj, Lj);
-		nsjj = nzj >> PECH_NS_SHIFT;
-		nzj &= PECH_NZ_MASK;
-		jj = j;
-		pjj = pj;
-		nzjj = nzj;
-		const uint32_t rr = r0 - pj;
-#ifdef PECH_LR4_LAZY // A/B: no speculative row offsets (a whole 4 KiB per wave through the TA at entry)
-		if (lane * 16u < nzj) {
-#else
-		if (j != cg && lane * 16u < nzj) { // speculation missed: the start chunk's row offsets now
-#endif
-#pragma unroll
-			for (uint32_t k = 0; k < 4; ++k)
-				lr4[k] = ((const u32x4 *)(lrs + j * PECH_CHUNK + lane * 16u))[k];
-		}
-		// position: the count of the chunk's offsets <= rr (nondecreasing
-		// over its nz non-empty cores), and the row inside that buffer
-		uint32_t c2 = 0, lo = 0;
-#pragma unroll
-		for (uint32_t k = 0; k < 16; ++k) {
-			const uint32_t e = lr4[k >> 2][k & 3u];
-			const bool ok = lane * 16u + k < nzj && e <= rr;
-			c2 += ok ? 1u : 0u;
-			lo = ok ? max(lo, e) : lo;
-		}
-		// (offsets increase over the non-empty cores: the lanes with c2 > 0
-		// are a prefix, and the last of them holds the largest offset <= rr)
-		const uint32_t Lp = last_lane_with(c2);
-		const uint32_t cpos = Lp * 16u + lane_value(c2, Lp);
-		p0 = j * PECH_CHUNK + cpos - 1u;
-		lr0 = rr - lane_value(lo, Lp);
-#ifdef PECH_DEBUG_BOUNDS
-		if (lane == 0 && (j >= nchunks || cpos == 0 || cpos > nzj || lr0 >= cores[p0].rows))
-			printf("PECH OOB prologue blk %u wave %u r0 %u j %u cg %u nchunks %u nzj %u cpos %u rr %u rows %u\n",
-			       blockIdx.x, wave, r0, j, cg, nchunks, nzj, cpos, rr, cores[min(p0, nchunks * PECH_CHUNK - 1u)].rows);
-#endif
-	}
 	// Static shares (no pool): the small cores of a chunk (its first nsjj
 	// positions) are walked in whole steps of 8 positions on a grid from the
 	// chunk start, each by the wave whose share holds the step's middle row
@@ -1730,6 +1822,9 @@ __device__ __forceinline__ void direct_body(uint32_t *lds, const pech_desc *__re
 					    const uint64_t *__restrict__ dsts = nullptr)
 {
 	const uint32_t tid = threadIdx.x;
+#ifdef PECH_KARGS_AT_ENTRY
+	asm volatile("" ::"s"(descs), "s"(n), "s"(consts), "s"(out), "s"(dsts)); // one kernarg round (main_body)
+#endif
 	const uint32_t lane = tid & 63u, g8 = tid & 7u, grp = lane >> 3;
 	const uint32_t lreg = ((lane & 31u) << 2) | (1u << 16);
 	const uint32_t wave = uni(tid >> 6);

@@ -1125,6 +1125,33 @@ __global__ __launch_bounds__(1024, 1) void k_fill(const uint32_t *tab, const uin
 		out[tid] = acc;
 }
 
+// instruction-fetch probe: the same count of VALU instructions as straight-
+// line code (NI x 8-byte v_add3_u32, cold in the instruction cache at every
+// dispatch?) or as a loop over 256 of them (2 KiB of code)
+template <int NI, bool LOOP>
+__global__ __launch_bounds__(1024) void k_code(uint32_t *out)
+{
+	uint32_t a = threadIdx.x, b = blockIdx.x, c = 7u;
+#define ADD3_8 "v_add3_u32 %0, %0, %1, %2\n" "v_add3_u32 %0, %0, %1, %2\n" "v_add3_u32 %0, %0, %1, %2\n" \
+	"v_add3_u32 %0, %0, %1, %2\n" "v_add3_u32 %0, %0, %1, %2\n" "v_add3_u32 %0, %0, %1, %2\n" \
+	"v_add3_u32 %0, %0, %1, %2\n" "v_add3_u32 %0, %0, %1, %2\n"
+#define ADD3_64 ADD3_8 ADD3_8 ADD3_8 ADD3_8 ADD3_8 ADD3_8 ADD3_8 ADD3_8
+	if (LOOP) {
+#pragma unroll 1
+		for (int it = 0; it < NI / 256; ++it) {
+#pragma unroll
+			for (int i = 0; i < 4; ++i)
+				asm volatile(ADD3_64 : "+v"(a) : "v"(b), "v"(c));
+		}
+	} else {
+#pragma unroll
+		for (int i = 0; i < NI / 64; ++i)
+			asm volatile(ADD3_64 : "+v"(a) : "v"(b), "v"(c));
+	}
+	if (a == 0x12345678u)
+		out[threadIdx.x] = a;
+}
+
 // usage: sched_probe [reps] [all|read|copy] [MiB per launch, default 1024]
 // (read: the static read stream only)
 int main(int argc, char **argv)
@@ -1562,6 +1589,33 @@ int main(int argc, char **argv)
 				}
 				printf("%s  {\"probe\": \"%s\", \"MiB\": %d, \"us\": %.2f, \"GBps\": %.1f}", sep(), names[v], mib,
 				       tot / reps * 1e3, sz ? sz / (tot / reps * 1e-3) / 1e9 : 0.0);
+			}
+	}
+	if (!strcmp(which, "icache")) {
+		hipEvent_t a0, a1;
+		CHECK(hipEventCreate(&a0));
+		CHECK(hipEventCreate(&a1));
+		for (int threads = 256; threads <= 1024; threads *= 4)
+			for (int v = 0; v < 6; ++v) {
+				float tot = 0;
+				for (int r = -2; r < reps; ++r) {
+					switch (v) {
+					case 0: hipExtLaunchKernelGGL((k_code<1024, false>), dim3(ncu), dim3(threads), 0, 0, a0, a1, 0, out); break;
+					case 1: hipExtLaunchKernelGGL((k_code<1024, true>), dim3(ncu), dim3(threads), 0, 0, a0, a1, 0, out); break;
+					case 2: hipExtLaunchKernelGGL((k_code<4096, false>), dim3(ncu), dim3(threads), 0, 0, a0, a1, 0, out); break;
+					case 3: hipExtLaunchKernelGGL((k_code<4096, true>), dim3(ncu), dim3(threads), 0, 0, a0, a1, 0, out); break;
+					case 4: hipExtLaunchKernelGGL((k_code<8192, false>), dim3(ncu), dim3(threads), 0, 0, a0, a1, 0, out); break;
+					default: hipExtLaunchKernelGGL((k_code<8192, true>), dim3(ncu), dim3(threads), 0, 0, a0, a1, 0, out); break;
+					}
+					CHECK(hipEventSynchronize(a1));
+					float ms;
+					CHECK(hipEventElapsedTime(&ms, a0, a1));
+					if (r >= 0)
+						tot += ms;
+				}
+				static const int ni[] = {1024, 1024, 4096, 4096, 8192, 8192};
+				printf("%s  {\"probe\": \"%d VALU instrs, %s\", \"threads\": %d, \"code_KiB\": %d, \"us\": %.2f}", sep(), ni[v],
+				       v & 1 ? "loop of 256" : "straight-line", threads, v & 1 ? 2 : ni[v] * 8 / 1024, tot / reps * 1e3);
 			}
 	}
 	if (!strcmp(which, "grid")) { // the best shapes measured: one float4 per thread, non-persistent grid, nt
