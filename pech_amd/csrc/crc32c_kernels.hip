@@ -48,8 +48,8 @@
 #define PECH_MAIN_THREADS (64u * PECH_MAIN_WAVES)
 // Diagnostic switches that change results exist only with PECH_DIAG (A/B
 // builds, tools/build_ab.sh): a product build that sees one fails here.
-#if (defined(PECH_AB_NOLDS) || defined(PECH_AB_NOLOAD) || defined(PECH_AB_NOATOMIC)) && !defined(PECH_DIAG)
-#error "PECH_AB_NOLDS / PECH_AB_NOLOAD / PECH_AB_NOATOMIC produce wrong CRCs: diagnostic builds must also define PECH_DIAG"
+#if (defined(PECH_AB_NOLDS) || defined(PECH_AB_NOLOAD) || defined(PECH_AB_NOATOMIC) || defined(PECH_AB_NOSHIFT)) && !defined(PECH_DIAG)
+#error "PECH_AB_NOLDS / PECH_AB_NOLOAD / PECH_AB_NOATOMIC / PECH_AB_NOSHIFT produce wrong CRCs: diagnostic builds must also define PECH_DIAG"
 #endif
 
 // Split-step results are XORed into a workgroup table in LDS and reach out[]
@@ -178,6 +178,10 @@ __device__ __forceinline__ uint32_t adv_tab(const uint32_t *lds, uint32_t tab, u
 // v * x^(8m) mod P with the 64-ary power table POWB[i][j] = x^(8 j 64^i)
 __device__ __forceinline__ uint32_t shift_bytes(const uint32_t *powb, uint64_t m, uint32_t v)
 {
+#ifdef PECH_AB_NOSHIFT // diagnostic build only: the run-end shifts skipped (wrong CRCs)
+	if (m != 0x9E3779B9u)
+		return v;
+#endif
 #pragma unroll
 	for (uint32_t i = 0; i < 6; ++i) {
 		const uint32_t d = (uint32_t)(m >> (6u * i)) & 63u;
@@ -1268,6 +1272,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifndef PECH_CONSTS_LAST
 	load_consts();
 #endif
+	const uint32_t rows0 = uni(partials[0]); // chunk 0's rows (the early fill's launch-size estimate)
 	// the speculative start (below), its chunk's row offsets, then the chunk totals
 	u32x4 lr4[4];
 	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
@@ -1303,12 +1308,59 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	load_consts();
 #endif
 	STAMP(t_issued);
+	// The LDS tables.  A_128 once per bank: its 32 copies as 8 x 16 B; lane t
+	// starts at copy group t mod 8 so neighbouring lanes, whose rows are
+	// 256 B apart, write different banks.  Then the single-copy tables and
+	// the empty deferral table.
+	auto fill_tables = [&](bool il_tab) {
+#pragma unroll
+		for (uint32_t j = 0; j < T128; ++j) {
+			const uint32_t w = tid + j * PECH_MAIN_THREADS, k = w >> 8, e = w & 0xFFu;
+			const u32x4 v = (u32x4)(il_tab ? t16k[j] : t128[j]);
+			char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+#pragma unroll
+			for (uint32_t q = 0; q < 8u; ++q)
+				*(u32x4 *)(dst + 16u * ((q + w) & 7u)) = v;
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < TPT; ++k)
+			if (tid + k * PECH_MAIN_THREADS < NT4)
+				*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
+		if (tid < 128u)
+			lds[L_XINV / 4u + tid] = txi;
+		if (tid == 0)
+			lds[L_POOL / 4u] = 0u;
+		if (tid < PECH_DEFER_SLOTS) {
+			lds[L_DEFER / 4u + tid] = PECH_DEFER_EMPTY;
+			lds[L_DEFER / 4u + PECH_DEFER_SLOTS + tid] = 0u;
+			if (tid == 0)
+				lds[L_DEFER_DONE / 4u] = 0u;
+		}
+	};
 
 	// The chunk scan and the start search (prologue_start): four chunks per
 	// lane for batches of up to 256 chunks (262,144 buffers), sixteen beyond.
 	// Every wave of the CU runs it, so its instruction count is the prologue's
 	// cost: a wave64 VALU instruction issues every 4 cycles per SIMD and four
 	// waves share a SIMD (the 16-per-lane loops alone were ~1 us of it).
+	// Launches of up to about PECH_EARLY_FILL_ROWS rows per workgroup (128
+	// MiB on 256 CUs; estimated from chunk 0's rows, exact for uniform
+	// batches): the CRC kernel (one table set) writes and publishes the LDS
+	// tables as soon as they arrive -- with the chunk totals the scan waits
+	// for -- and each wave then streams as soon as its own prime lands.  With
+	// the barrier after the prime every wave waits for the workgroup's
+	// slowest prologue: 4 MiB launches 25.4 -> 21.7 us.  Larger launches keep
+	// it, fill included: there a fill before the scan cost +1.2 us per
+	// launch, and without the barrier the early starters took issue slots
+	// from the waves still in their prologue and the tail grew
+	// (profiles/r04/ab_early_fill.txt).  The copy kernel's table depends on
+	// the scan (interleaved mode): late fill.
+	const bool early_fill = !COPY && !PECH_IL_CRC &&
+				(uint64_t)rows0 * nchunks <= (uint64_t)PECH_EARLY_FILL_ROWS * gridDim.x; // workgroup-uniform
+	if (early_fill) {
+		fill_tables(false);
+		__syncthreads();
+	}
 	Start sv;
 	const bool live = nchunks <= 64u * 4u
 			  ? prologue_start<COPY, 4>(lds, cores, lrs, partials, nzs, n, nchunks, lane, wave, W, rpw_min, pg,
@@ -1366,36 +1418,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	if (S.T)
 		RING_PRIME_RS(S, ring, rsb);
 
-	// The LDS tables, needed from the first row on, written while the prime
-	// is in flight.  A_128 once per bank: its 32 copies as 8 x 16 B; lane t
-	// starts at copy group t mod 8 so neighbouring lanes, whose rows are
-	// 256 B apart, write different banks.  Then the single-copy tables and
-	// the empty deferral table.
-#pragma unroll
-	for (uint32_t j = 0; j < T128; ++j) {
-		const uint32_t w = tid + j * PECH_MAIN_THREADS, k = w >> 8, e = w & 0xFFu;
-		const u32x4 v = (u32x4)(il ? t16k[j] : t128[j]);
-		char *dst = (char *)lds + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
-#pragma unroll
-		for (uint32_t q = 0; q < 8u; ++q)
-			*(u32x4 *)(dst + 16u * ((q + w) & 7u)) = v;
-	}
-#pragma unroll
-	for (uint32_t k = 0; k < TPT; ++k)
-		if (tid + k * PECH_MAIN_THREADS < NT4)
-			*(u32x4 *)((char *)lds + L_TAB4 + 16u * (tid + k * PECH_MAIN_THREADS)) = tv[k];
-	if (tid < 128u)
-		lds[L_XINV / 4u + tid] = txi;
-	if (tid == 0)
-		lds[L_POOL / 4u] = 0u;
-	if (tid < PECH_DEFER_SLOTS) {
-		lds[L_DEFER / 4u + tid] = PECH_DEFER_EMPTY;
-		lds[L_DEFER / 4u + PECH_DEFER_SLOTS + tid] = 0u;
-		if (tid == 0)
-			lds[L_DEFER_DONE / 4u] = 0u;
-	}
+	// otherwise the tables are written while the prime is in flight
+	if (!early_fill)
+		fill_tables(il);
 	STAMP(t_fill);
-	__syncthreads(); // tables published; every wave's prime is already in flight
+	if (!early_fill)
+		__syncthreads(); // tables published; every wave's prime is already in flight
 	STAMP(t_start);
 	// the wave's first pool claim, one item ahead (resolved when its first
 	// item is done)
@@ -1547,7 +1575,13 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				S.nu = 0;
 		}
 #endif
+#ifdef PECH_STAMP_FIN // stamps build: the last step's fold + shift (75 % stamp -> its start)
+		tq[2] = __builtin_amdgcn_s_memrealtime();
+#endif
 		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));
+#ifdef PECH_STAMP_FIN
+		tq[1] = __builtin_amdgcn_s_memrealtime();
+#endif
 		S = N;
 #ifdef PECH_STAMPS
 		++nstep;
@@ -2062,6 +2096,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.22 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 U" PECH_STR(
+	return "pech_crc32c 0.23 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -49,6 +49,9 @@
 #ifndef PECH_IL_COPY
 #define PECH_IL_COPY 1            /* fused copy's interleaved mode (profiles/r03/ab_copy_interleaved.txt) */
 #endif
+#ifndef PECH_EARLY_FILL_ROWS
+#define PECH_EARLY_FILL_ROWS 4096u /* CRC kernel: tables published before the start search up to this many rows per workgroup */
+#endif
 #ifndef PECH_IL_CRC
 #define PECH_IL_CRC 0             /* the same for the CRC-only kernel (A/B: reads gained nothing in the probe) */
 #endif

@@ -167,7 +167,7 @@ def _hipcc():
     return hipcc
 
 
-@pytest.mark.parametrize("flag", ["-DPECH_AB_NOLDS", "-DPECH_AB_NOLOAD", "-DPECH_AB_NOATOMIC"])
+@pytest.mark.parametrize("flag", ["-DPECH_AB_NOLDS", "-DPECH_AB_NOLOAD", "-DPECH_AB_NOATOMIC", "-DPECH_AB_NOSHIFT"])
 def test_result_changing_switches_need_pech_diag(flag):
     # a stray diagnostic -D must not build a library that returns wrong CRCs
     r = subprocess.run([_hipcc(), "-E", "--offload-arch=gfx950", "--cuda-device-only", flag, SRC, "-o", os.devnull],

@@ -70,6 +70,11 @@ print("mean wave busy / span: %.3f" % float(((e - s) / span).mean()))
 busy = (e - s) / 100
 print("busy us p1/p10/p50/p90/p99/max: %.1f %.1f %.1f %.1f %.1f %.1f" % (pct(busy, 1), pct(busy, 10), pct(busy, 50),
                                                                         pct(busy, 90), pct(busy, 99), busy.max()))
+if os.environ.get("PECH_STAMP_FIN") == "1":  # stamps built with -DPECH_STAMP_FIN: q3/q2 bracket the last finish_run
+    fin, flush = (q2 - q3) / 100, (e - q2) / 100
+    print("last step's fold+shift us p10/p50/p90/max: %.2f %.2f %.2f %.2f" % (pct(fin, 10), pct(fin, 50), pct(fin, 90), fin.max()))
+    print("after it (deferral flush) us p50/p90/max: %.2f %.2f %.2f" % (pct(flush, 50), pct(flush, 90), flush.max()))
+    print("start->last fold us p10/p50/p90/max: %.1f %.1f %.1f %.1f" % tuple(x / 100 for x in (pct(q3 - s, 10), pct(q3 - s, 50), pct(q3 - s, 90), (q3 - s).max())))
 hist, edges = np.histogram(e / 100, bins=12)
 print("end-time histogram (us):", [(round(float(edges[i]),1), int(hist[i])) for i in range(len(hist))])
 
