@@ -40,6 +40,7 @@
 #include <dlfcn.h>
 #include <errno.h>
 #include <limits.h>
+#include <stdio.h>
 #include <linux/futex.h>
 #include <stdlib.h>
 #include <sys/syscall.h>
@@ -327,6 +328,33 @@ struct crc32c_async {
 	std::deque<Item> items;      // items[k] is submission id base + k
 	uint64_t base = 0;
 	int err = 0;                 // sticky failure of this context
+	// PECH_ASYNC_PROF=1: the calling thread's CPU ns per phase, printed by
+	// destroy (where a DMA-mode thread's time goes; measurement only)
+	bool prof = false;
+	uint64_t prof_ns[5] = {0, 0, 0, 0, 0}; // copies issued, kernels + D2H + host function, waits for a slot, submit, complete
+	uint64_t prof_launches = 0;
+};
+
+static inline uint64_t thread_ns()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+// adds the calling thread's CPU time in its scope to a->prof_ns[k]
+struct ProfScope {
+	crc32c_async *a;
+	int k;
+	uint64_t t0;
+	ProfScope(crc32c_async *ctx, int kind) : a(ctx->prof ? ctx : nullptr), k(kind), t0(a ? thread_ns() : 0) {}
+	void stop()
+	{
+		if (a)
+			a->prof_ns[k] += thread_ns() - t0;
+		a = nullptr;
+	}
+	~ProfScope() { stop(); }
 };
 
 static void slot_free(Slot *s)
@@ -502,7 +530,11 @@ static int get_slot(crc32c_async *a, Slot **out)
 	}
 	// every slot in flight: wait for the oldest (callbacks still run only
 	// in crc32c_async_complete)
-	int rc = reap(a, true);
+	int rc;
+	{
+		ProfScope ps(a, 2);
+		rc = reap(a, true);
+	}
 	if (rc)
 		return rc;
 	return get_slot(a, out);
@@ -530,6 +562,8 @@ static int launch_slot(crc32c_async *a)
 	if (!s || s->pieces.empty())
 		return 0;
 	const unsigned m = (unsigned)s->pieces.size();
+	a->prof_launches++;
+	ProfScope ps_copies(a, 0);
 	if (!s->dma.empty()) {
 		hipError_t e = hipErrorInvalidValue;
 		if (!pech_fault(PECH_FAULT_ASYNC_DMA)) {
@@ -570,6 +604,8 @@ static int launch_slot(crc32c_async *a)
 			fail_cur_slot(a, -EIO));
 		descs = s->d_desc;
 	}
+	ps_copies.stop();
+	ProfScope ps_launch(a, 1);
 	s->finished.store(0, std::memory_order_relaxed);
 	if (pech_fault(PECH_FAULT_ASYNC_LAUNCH)) {
 		pech_internal_set_err("crc32c_async: injected launch failure (test)");
@@ -612,6 +648,8 @@ static struct crc32c_async *async_create(unsigned int flags)
 		crc32c_async_destroy(a);
 		return nullptr;
 	}
+	const char *pf = getenv("PECH_ASYNC_PROF");
+	a->prof = pf && pf[0] == '1';
 	a->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
 	if (a->efd < 0) {
 		pech_internal_set_err("crc32c_async_create: eventfd: %s", strerror(errno));
@@ -735,6 +773,7 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 	}
 	if (a->err)
 		return a->err;
+	ProfScope ps(a, 3);
 	return on_lib_stack([&] { return async_submit(a, buf, len, seed, done, arg); });
 }
 
@@ -776,6 +815,7 @@ extern "C" int crc32c_async_complete(struct crc32c_async *a)
 {
 	if (!a)
 		return -EINVAL;
+	ProfScope ps(a, 4);
 	const int rc = on_lib_stack([&] {
 		uint64_t cnt;
 		while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
@@ -827,6 +867,12 @@ extern "C" void crc32c_async_destroy(struct crc32c_async *a)
 			slot_free(s); // synchronises the slot's stream first
 		return 0;
 	});
+	if (a->prof)
+		fprintf(stderr,
+			"{\"async_prof\": {\"launches\": %llu, \"thread_cpu_us\": {\"copies\": %.1f, \"launch\": %.1f, "
+			"\"slot_wait\": %.1f, \"submit\": %.1f, \"complete\": %.1f}}}\n",
+			(unsigned long long)a->prof_launches, a->prof_ns[0] / 1e3, a->prof_ns[1] / 1e3, a->prof_ns[2] / 1e3,
+			a->prof_ns[3] / 1e3, a->prof_ns[4] / 1e3);
 	if (a->efd >= 0)
 		close(a->efd);
 	delete a;
