@@ -175,6 +175,27 @@ __device__ __forceinline__ uint32_t adv_tab(const uint32_t *lds, uint32_t tab, u
 	return xor3(t[v & 0xFFu], t[256u + ((v >> 8) & 0xFFu)], t[512u + ((v >> 16) & 0xFFu)] ^ t[768u + (v >> 24)]);
 }
 
+// a * b mod P on the GPU, five VALU ops per bit of a: the bit of a as a
+// mask (v_bfe_i32), p ^= b & mask and b = b*x as one v_bitop3 each (0x78:
+// S0 ^ (S1 & S2)), with the shift and the carry mask of b.  The generic loop
+// of gf2.h compiles to seven; the run-end shifts are ~1 us of every split
+// step (profiles/r04/ab_shift_early.txt).
+__device__ __forceinline__ uint32_t gf2_mulmod_dev(uint32_t a, uint32_t b)
+{
+#ifdef PECH_MULMOD_GENERIC // A/B: the gf2.h loop
+	return gf2_mulmod(a, b);
+#endif
+	uint32_t p = 0;
+#pragma unroll
+	for (int i = 31; i >= 0; --i) {
+		const uint32_t ma = (uint32_t)((int32_t)(a << (31 - i)) >> 31);
+		p = __builtin_amdgcn_bitop3_b32(p, b, ma, 0x78);
+		const uint32_t mb = (uint32_t)((int32_t)(b << 31) >> 31);
+		b = __builtin_amdgcn_bitop3_b32(b >> 1, mb, CRC32C_POLY_REFLECTED, 0x78);
+	}
+	return p;
+}
+
 // v * x^(8m) mod P with the 64-ary power table POWB[i][j] = x^(8 j 64^i)
 __device__ __forceinline__ uint32_t shift_bytes(const uint32_t *powb, uint64_t m, uint32_t v)
 {
@@ -186,7 +207,7 @@ __device__ __forceinline__ uint32_t shift_bytes(const uint32_t *powb, uint64_t m
 	for (uint32_t i = 0; i < 6; ++i) {
 		const uint32_t d = (uint32_t)(m >> (6u * i)) & 63u;
 		if (d)
-			v = gf2_mulmod(powb[64u * i + d], v);
+			v = gf2_mulmod_dev(powb[64u * i + d], v);
 	}
 	return v;
 }
@@ -918,7 +939,7 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 	uint32_t v = 0;
 	if (active && g8 == 0) // m < 0: the run's trailing virtual zeros outweigh the tail
 		v = m > 0 ? shift_bytes(lds + L_POWB / 4u, (uint64_t)m, u)
-			  : (m < 0 ? gf2_mulmod(lds[L_XINV / 4u + (uint32_t)(-m)], u) : u);
+			  : (m < 0 ? gf2_mulmod_dev(lds[L_XINV / 4u + (uint32_t)(-m)], u) : u);
 	// A split step (every active group on one buffer) folds its 8 group
 	// results in registers: one atomic per wave instead of 8 on one address.
 	const uint32_t o0 = uni(orig);
@@ -1823,7 +1844,7 @@ __device__ __forceinline__ void finish_direct(uint32_t *lds, uint32_t g8, uint32
 	uint32_t v = 0;
 	if (S.nu != 0u && lead) {
 		const uint32_t tr = DSTEP_TRAIL(S);
-		v = tr ? gf2_mulmod(lds[L_XINV / 4u + tr], u) : u;
+		v = tr ? gf2_mulmod_dev(lds[L_XINV / 4u + tr], u) : u;
 	}
 	const bool slow = STEP_SLOW(S) != 0u && lead;
 	if (__ballot(slow) != 0ull && slow) { // the rare slow path: its load waits for the ring too
@@ -2096,6 +2117,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.23 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.24 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }
