@@ -94,6 +94,13 @@ static void build_consts(uint32_t *c)
 			for (uint32_t e = 0; e < 256; ++e)
 				c[PECH_C_TAB16K + k * 256u + e] = gf2_mulmod(xk, e << (8 * k));
 	}
+	// ROWPOW[k] = x^(8 * 128 k) = A_128^k(1), by the A_128 byte tables
+	c[PECH_C_ROWPOW] = CRC32C_ONE;
+	for (uint32_t k = 1; k < PECH_ROWPOW_N; ++k) {
+		const uint32_t v = c[PECH_C_ROWPOW + k - 1];
+		c[PECH_C_ROWPOW + k] = c[PECH_C_TAB128 + (v & 0xFFu)] ^ c[PECH_C_TAB128 + 256u + ((v >> 8) & 0xFFu)] ^
+				       c[PECH_C_TAB128 + 512u + ((v >> 16) & 0xFFu)] ^ c[PECH_C_TAB128 + 768u + (v >> 24)];
+	}
 	// XINV[k] = x^(-8k): undoes k trailing zero bytes (a core's last line)
 	const uint32_t xinv8 = gf2_xinv8n(1);
 	uint32_t acc = CRC32C_ONE;

@@ -875,6 +875,11 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 #define STEP_ZL(S) ((S).oz & (1u << 27)) // bit 28: STEP_SLOW (direct kernel), bit 29: PECH_OZ_RA25
 #define STEP_RA(S) ((uint64_t)((S).mp >> 7) | (uint64_t)((S).oz & PECH_OZ_RA25) >> 4) // rows after the run
 #define STEP_M(S) ((int64_t)(STEP_RA(S) * PECH_ROW_BYTES + ((S).mp & 15u)) - (int64_t)((S).mp & 0x70u))
+// x^(8 * 128 * rows after the run), modulo the table's span (finish_run)
+__device__ __forceinline__ uint32_t rowpow(const uint32_t *consts, const Step &S)
+{
+	return consts[PECH_C_ROWPOW + ((uint32_t)STEP_RA(S) & (PECH_ROWPOW_N - 1u))];
+}
 
 // a / b with a 32-bit quotient: one 32-bit division when a fits 32 bits
 // (wave-uniform: a scalar branch), the 64-bit sequence otherwise
@@ -922,8 +927,10 @@ __device__ __forceinline__ void horner_row_pred(const uint32_t *lds, uint32_t lr
 // Fold a group's 32 stream registers into the CRC of its run (as a message
 // ending at the run's last row), shift it to the buffer's core end plus the
 // tail (m bytes), xor into out[orig].
+template <bool ROWPOW>
 __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t s0, uint32_t s1, uint32_t s2,
-					   uint32_t s3, int64_t m, bool active, uint32_t *out, uint32_t orig)
+					   uint32_t s3, int64_t m, uint64_t ra, uint32_t tpow, bool active, uint32_t *out,
+					   uint32_t orig)
 {
 	uint32_t u = adv_tab(lds, L_TAB4, s0) ^ s1;
 	u = adv_tab(lds, L_TAB4, u) ^ s2;
@@ -937,9 +944,26 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 	u = adv_tab(lds, L_TAB32, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x102, 0xf, 0xf, true);
 	u = adv_tab(lds, L_TAB64, u) ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x104, 0xf, 0xf, true);
 	uint32_t v = 0;
-	if (active && g8 == 0) // m < 0: the run's trailing virtual zeros outweigh the tail
+	if (ROWPOW) {
+		// m = 128 ra + dl, dl in [-112, 15]: x^(8 dl) from the power table
+		// (x^(-8k) for the trailing virtual zeros), x^(8 128 ra) read from
+		// the row-power table one step ahead (tpow) -- at most two products,
+		// one for aligned buffers, instead of one per 6-bit digit of m (up to
+		// four for a 4 MiB buffer)
+		if (active && g8 == 0) {
+			const int32_t dl = (int32_t)(m - (int64_t)(ra * PECH_ROW_BYTES));
+			v = u;
+			if (dl != 0)
+				v = gf2_mulmod_dev(dl > 0 ? lds[L_POWB / 4u + (uint32_t)dl] : lds[L_XINV / 4u + (uint32_t)(-dl)], v);
+			if (ra != 0)
+				v = gf2_mulmod_dev(tpow, v);
+			if (ra >> PECH_ROWPOW_BITS) // buffers above 32 MiB: the rest by digits
+				v = shift_bytes(lds + L_POWB / 4u, (ra >> PECH_ROWPOW_BITS) << (PECH_ROWPOW_BITS + 7u), v);
+		}
+	} else if (active && g8 == 0) { // m < 0: the run's trailing virtual zeros outweigh the tail
 		v = m > 0 ? shift_bytes(lds + L_POWB / 4u, (uint64_t)m, u)
 			  : (m < 0 ? gf2_mulmod_dev(lds[L_XINV / 4u + (uint32_t)(-m)], u) : u);
+	}
 	// A split step (every active group on one buffer) folds its 8 group
 	// results in registers: one atomic per wave instead of 8 on one address.
 	const uint32_t o0 = uni(orig);
@@ -1436,6 +1460,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	Step S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
 		    : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
 	STAMP(t_plan);
+	uint32_t tpow = COPY ? 0u : rowpow(consts, S); // x^(8 128 ra) of the step's run (finish_run)
 	if (S.T)
 		RING_PRIME_RS(S, ring, rsb);
 
@@ -1556,6 +1581,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		}
 		const Step N = il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 				  : plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
+		const uint32_t tpow_n = COPY ? 0u : rowpow(consts, N); // (used when N ends)
 		if constexpr (COPY) { // block discipline: this block's rows and stores, then the next step's loads
 			const bool more = N.T != 0;
 			const Step &L = more ? N : S;
@@ -1599,7 +1625,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifdef PECH_STAMP_FIN // stamps build: the last step's fold + shift (75 % stamp -> its start)
 		tq[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-		finish_run(lds, g8, s0, s1, s2, s3, STEP_M(S), S.nu != 0, out, STEP_ORIG(S));
+		finish_run<!COPY>(lds, g8, s0, s1, s2, s3, STEP_M(S), STEP_RA(S), tpow, S.nu != 0, out, STEP_ORIG(S));
+		tpow = tpow_n;
 #ifdef PECH_STAMP_FIN
 		tq[1] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2117,6 +2144,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.24 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.25 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -85,7 +85,10 @@
 #define PECH_C_TAB1 5504u   /* A_1 = the reference table, include/crc32c.h:16 */
 #define PECH_C_XINV 5760u   /* x^(-8k), k < 128 (trailing virtual zeros)      */
 #define PECH_C_TAB16K 5888u /* A_16384 byte tables (fused copy, interleaved rows) */
-#define PECH_C_WORDS 6912u
+#define PECH_C_ROWPOW 6912u /* x^(8*128*k), k < PECH_ROWPOW_N (run-end shifts by whole rows, global) */
+#define PECH_ROWPOW_BITS 18u
+#define PECH_ROWPOW_N (1u << PECH_ROWPOW_BITS) /* 1 MiB: shifts of up to 32 MiB in one table read */
+#define PECH_C_WORDS (PECH_C_ROWPOW + PECH_ROWPOW_N)
 
 /* device batch descriptor (matches struct crc32c_desc in include/) */
 struct pech_desc {
