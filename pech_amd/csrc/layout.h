@@ -65,7 +65,7 @@
 #define PECH_POOL_MIN_SHARE 1024u /* uniform batches pool only shares of at least this many rows */
 #endif
 #ifndef PECH_POOL_ROWS
-#define PECH_POOL_ROWS 512u       /* uniform batches: at most this many of a wave's rows are pooled */
+#define PECH_POOL_ROWS 1536u      /* uniform batches: at most this many of a wave's rows are pooled */
 #endif
 #define PECH_NZ_UNIFORM 0x80000000u /* nzs[] flag: every buffer of the chunk has a core of the same rows */
 #define PECH_NZ_MASK 0x7FFu         /* nzs[] bits 0-10: non-empty cores of the chunk */
