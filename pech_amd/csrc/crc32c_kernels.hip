@@ -598,6 +598,17 @@ __device__ __forceinline__ u32x4 keep_below(u32x4 v, uint32_t kb)
 	return r;
 }
 
+// one descriptor per lane group (a step's speculative descriptors)
+__device__ __forceinline__ pech_core load_spec(const pech_core *__restrict__ cores, uint32_t p)
+{
+	const u32x4 v = ((const u32x4 *)cores)[p];
+	pech_core c;
+	c.addr = ((uint64_t)v.y << 32) | v.x;
+	c.rows = v.z;
+	c.meta = v.w;
+	return c;
+}
+
 // Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
 // the destination offset of each group's buffer (deltas[orig], scalar loads).
 // PRE: `spec` holds cores[ppos + grp] (loaded at kernel entry); a step that
@@ -1326,13 +1337,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t pg = uni(min((uint32_t)((double)wglob * (double)n / (double)W), n - 1u));
 	const uint32_t cg = pg >> 10;                                   // and chunk
 	const uint32_t lrg = lrs[pg]; // pg's row offset in its chunk
-	pech_core spec; // cores[pg + grp] (pg + 7 may run into lrs: workspace memory, used only if in the chunk)
-	{
-		const u32x4 v = ((const u32x4 *)cores)[pg + grp];
-		spec.addr = ((uint64_t)v.y << 32) | v.x;
-		spec.rows = v.z;
-		spec.meta = v.w;
-	}
+	// cores[pg + grp] (pg + 7 may run into lrs: workspace memory, used only if in the chunk)
+	const pech_core spec = load_spec(cores, pg + grp);
 
 	// the speculative row offsets.  Unconditional -- a load under a branch
 	// gets a vmcnt(0) at the join -- with lanes past the chunk's buffers
@@ -1461,6 +1467,19 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		    : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
 	STAMP(t_plan);
 	uint32_t tpow = COPY ? 0u : rowpow(consts, S); // x^(8 128 ra) of the step's run (finish_run)
+	// Static shares walk on from where a step ends: the CRC kernel loads the
+	// 8 descriptors there (one per group, as `spec`) when it plans a step, so
+	// planning the step after it needs no dependent load (the copy kernel has
+	// no VGPRs to spare).  nslots - 1 clamps a cursor at the batch end (the
+	// 7 entries past it lie in lrs: workspace memory, never used).
+	const uint32_t nslots = nchunks * PECH_CHUNK;
+#ifndef PECH_NEXT_SPEC_FIRST
+	uint32_t nppos = 0xFFFFFFFFu; // (the first step's successor plans with loads)
+	pech_core nspec = pech_core{};
+#else // A/B: prefetched from the first step on
+	uint32_t nppos = COPY ? 0u : min(S.pos, nslots - 1u);
+	pech_core nspec = COPY ? pech_core{} : load_spec(cores, nppos + grp);
+#endif
 	if (S.T)
 		RING_PRIME_RS(S, ring, rsb);
 
@@ -1579,8 +1598,18 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				}
 			}
 		}
+#ifndef PECH_NO_NEXT_SPEC
+		const Step N = il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
+			   : COPY ? plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid)
+				  : plan_step<COPY, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid, nspec, nppos);
+		if (!COPY) { // the descriptors at N's end, for the step after it
+			nppos = min(N.pos, nslots - 1u);
+			nspec = load_spec(cores, nppos + grp);
+		}
+#else // A/B: N's descriptors loaded when N is planned
 		const Step N = il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 				  : plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
+#endif
 		const uint32_t tpow_n = COPY ? 0u : rowpow(consts, N); // (used when N ends)
 		if constexpr (COPY) { // block discipline: this block's rows and stores, then the next step's loads
 			const bool more = N.T != 0;
@@ -2144,6 +2173,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.26 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.27 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }
