@@ -1492,9 +1492,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	STAMP(t_start);
 	// the wave's first pool claim, one item ahead (resolved when its first
 	// item is done)
-	uint32_t claim = 0;
-	if (jmax > 1u && lane == 0)
+	uint32_t claim = 0, claim2 = 0;
+	if (jmax > 1u && lane == 0) {
 		claim = atomicAdd(lds + L_POOL / 4u, 1u);
+		if (!COPY) // the CRC kernel claims two items ahead: the second one's descriptors are prefetched
+			claim2 = atomicAdd(lds + L_POOL / 4u, 1u);
+	}
 #ifdef PECH_STAMPS
 	uint64_t tq[3] = {0, 0, 0};
 	uint32_t nstep = 0;
@@ -1588,8 +1591,14 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				const uint32_t a = (uint32_t)(wg0 + (uint64_t)wg_rows * sh / PECH_MAIN_WAVES);
 				const uint32_t b = (uint32_t)(wg0 + (uint64_t)wg_rows * (sh + 1u) / PECH_MAIN_WAVES);
 				const uint32_t st = share_head(a, b) + (j - 1u) * PECH_ITEM_ROWS;
-				if (lane == 0)
-					claim = atomicAdd(lds + L_POOL / 4u, 1u); // the next claim, one item ahead
+				if (COPY) {
+					if (lane == 0)
+						claim = atomicAdd(lds + L_POOL / 4u, 1u); // the next claim, one item ahead
+				} else {
+					claim = claim2; // (lane 0's)
+					if (lane == 0)
+						claim2 = atomicAdd(lds + L_POOL / 4u, 1u); // two items ahead
+				}
 				if (st < b) {
 					npos = st / U0;
 					nlr = st - npos * U0;
@@ -1602,8 +1611,18 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		const Step N = il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 			   : COPY ? plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid)
 				  : plan_step<COPY, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid, nspec, nppos);
-		if (!COPY) { // the descriptors at N's end, for the step after it
+		if (!COPY) { // the descriptors where the step after N starts
 			nppos = min(N.pos, nslots - 1u);
+			if (jmax > 1u && N.rem == 0) {
+				// N ends a pooled item: the next item is the pending claim's
+				// (a guess: an item past its share's end moves on to the next
+				// claim, and the plan then misses and loads)
+				const uint32_t c = uni(claim), j = 1u + (c >> 4), sh = c & 15u;
+				const uint32_t a = (uint32_t)(wg0 + (uint64_t)wg_rows * sh / PECH_MAIN_WAVES);
+				const uint32_t b = (uint32_t)(wg0 + (uint64_t)wg_rows * (sh + 1u) / PECH_MAIN_WAVES);
+				const uint32_t st = share_head(a, b) + (j - 1u) * PECH_ITEM_ROWS;
+				nppos = j < jmax && st < b ? min(st / U0, nslots - 1u) : nppos;
+			}
 			nspec = load_spec(cores, nppos + grp);
 		}
 #else // A/B: N's descriptors loaded when N is planned
@@ -2173,6 +2192,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.27 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.28 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }
