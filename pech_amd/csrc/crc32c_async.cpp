@@ -291,6 +291,7 @@ struct Slot {
 	size_t zc_bytes = 0; // bytes read in place: a slot launches at kSlotBytes of either
 	uint32_t maxlen = 0; // longest piece: the direct kernel takes slots of pieces below kDirectMax
 	bool inflight = false;
+	bool queued = false;      // CRC32C_ASYNC_DMA: filled, launched once the slots before it are harvested
 	bool inject_fail = false; // test build: this batch's stream "failed" (PECH_FAULT_ASYNC_STREAM)
 	uint64_t t_launch = 0;    // mono_ns() at launch
 };
@@ -322,6 +323,7 @@ struct crc32c_async {
 	bool ready = false; // fully created (destroy drains only then)
 	bool planned_only = false; // PECH_ASYNC_PLANNED=1: every slot on plan + main (A/B measurement)
 	size_t zc_max = kZeroCopyMax; // PECH_ASYNC_ZC_MAX=<bytes>: zero-copy threshold (A/B measurement)
+	unsigned max_slots = kMaxSlots; // PECH_ASYNC_SLOTS=<1..4>: slots in flight (A/B measurement)
 	std::vector<Slot *> slots;
 	std::deque<Slot *> inflight; // launch order
 	Slot *cur = nullptr;         // slot being filled
@@ -454,14 +456,36 @@ static void harvest(crc32c_async *a, Slot *s, int err)
 	s->zc_bytes = 0;
 	s->maxlen = 0;
 	s->inflight = false;
+	s->queued = false;
 	s->inject_fail = false;
 }
+
+static int issue_slot(crc32c_async *a, Slot *s);
 
 // Harvest finished slots (blocking on the oldest when `wait`), in order.
 static int reap(crc32c_async *a, bool wait_oldest, DeviceGuard *dg = nullptr)
 {
 	while (!a->inflight.empty()) {
 		Slot *s = a->inflight.front();
+		if (s->queued) { // CRC32C_ASYNC_DMA: the slots before it are harvested, so it launches now
+			if (a->err) { // (a sticky error: it never launches)
+				a->inflight.pop_front();
+				harvest(a, s, a->err);
+				if (wait_oldest)
+					return a->err;
+				continue;
+			}
+			if (dg && !dg->ensure())
+				return 0;
+			const int rc = issue_slot(a, s);
+			if (rc) {
+				if (wait_oldest)
+					return rc;
+				continue;
+			}
+			if (!wait_oldest)
+				return 0; // just launched
+		}
 		hipError_t q = hipSuccess;
 		if (wait_oldest) {
 			// sleep until the host function marks the slot; a failed stream
@@ -520,7 +544,7 @@ static int get_slot(crc32c_async *a, Slot **out)
 			a->cur = *out = s;
 			return 0;
 		}
-	if (a->slots.size() < kMaxSlots) {
+	if (a->slots.size() < a->max_slots) {
 		Slot *s = slot_new(a->efd);
 		if (!s)
 			return -ENOMEM;
@@ -556,11 +580,26 @@ static int fail_cur_slot(crc32c_async *a, int err)
 	return err;
 }
 
-static int launch_slot(crc32c_async *a)
+// A slot that cannot be launched: the one being filled (fail_cur_slot), or
+// a queued one, which is the oldest in flight when reap() launches it.
+static int fail_slot(crc32c_async *a, Slot *s, int err)
 {
-	Slot *s = a->cur;
-	if (!s || s->pieces.empty())
-		return 0;
+	if (s == a->cur)
+		return fail_cur_slot(a, err);
+	if (!a->inflight.empty() && a->inflight.front() == s)
+		a->inflight.pop_front();
+	harvest(a, s, err);
+	a->err = err;
+	const uint64_t one = 1;
+	ssize_t r = write(a->efd, &one, sizeof(one));
+	(void)r;
+	return err;
+}
+
+// Copies, descriptors, kernels, results and the host function of slot s:
+// the slot being filled, or a queued one (CRC32C_ASYNC_DMA, from reap()).
+static int issue_slot(crc32c_async *a, Slot *s)
+{
 	const unsigned m = (unsigned)s->pieces.size();
 	a->prof_launches++;
 	ProfScope ps_copies(a, 0);
@@ -591,17 +630,17 @@ static int launch_slot(crc32c_async *a)
 		}
 		if (e != hipSuccess) {
 			pech_internal_set_err("crc32c_async: payload DMA failed: %s", hipGetErrorString(e));
-			return fail_cur_slot(a, -EIO);
+			return fail_slot(a, s, -EIO);
 		}
 	}
 	for (auto &r : s->packed)
 		TRY_HIP(hipMemcpyAsync(s->d_stage + r.first, s->h_stage + r.first, r.second - r.first,
 				       hipMemcpyHostToDevice, s->stream),
-			fail_cur_slot(a, -EIO));
+			fail_slot(a, s, -EIO));
 	const pech_desc *descs = s->desc_view;
 	if (!descs) {
 		TRY_HIP(hipMemcpyAsync(s->d_desc, s->h_desc, m * sizeof(pech_desc), hipMemcpyHostToDevice, s->stream),
-			fail_cur_slot(a, -EIO));
+			fail_slot(a, s, -EIO));
 		descs = s->d_desc;
 	}
 	ps_copies.stop();
@@ -609,23 +648,48 @@ static int launch_slot(crc32c_async *a)
 	s->finished.store(0, std::memory_order_relaxed);
 	if (pech_fault(PECH_FAULT_ASYNC_LAUNCH)) {
 		pech_internal_set_err("crc32c_async: injected launch failure (test)");
-		return fail_cur_slot(a, -EIO);
+		return fail_slot(a, s, -EIO);
 	}
 	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream,
 				      s->maxlen < kDirectMax && !a->planned_only);
 	if (rc)
-		return fail_cur_slot(a, rc);
-	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), fail_cur_slot(a, -EIO));
+		return fail_slot(a, s, rc);
+	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), fail_slot(a, s, -EIO));
 	// test build: a batch whose stream fails after the launch -- HIP then
 	// skips its host function, so the eventfd stays quiet
 	s->inject_fail = pech_fault(PECH_FAULT_ASYNC_STREAM);
 	if (!s->inject_fail)
-		TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_cur_slot(a, -EIO));
-	s->inflight = true;
+		TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_slot(a, s, -EIO));
 	s->t_launch = mono_ns();
-	a->inflight.push_back(s);
-	a->cur = nullptr;
+	if (s->queued) {
+		s->queued = false; // (already in a->inflight, in order)
+	} else {
+		s->inflight = true;
+		a->inflight.push_back(s);
+		a->cur = nullptr;
+	}
 	return 0;
+}
+
+static int launch_slot(crc32c_async *a)
+{
+	Slot *s = a->cur;
+	if (!s || s->pieces.empty())
+		return 0;
+	if ((a->flags & CRC32C_ASYNC_DMA) && !a->inflight.empty()) {
+		// One slot's copies in flight at a time: with more, the runtime's
+		// copy calls spin on the caller's thread (36-70 us of its CPU per
+		// 4 MiB payload at 2-4 slots, 5 us at one; and 28-37 against 43
+		// GiB/s; profiles/r04/async_dma_slots.txt).  The filled slot waits,
+		// without a HIP call, until reap() has harvested the ones before it
+		// -- complete() runs on the eventfd their host functions write.
+		s->queued = true;
+		s->inflight = true;
+		a->inflight.push_back(s);
+		a->cur = nullptr;
+		return 0;
+	}
+	return issue_slot(a, s);
 }
 
 static struct crc32c_async *async_create(unsigned int flags)
@@ -643,6 +707,10 @@ static struct crc32c_async *async_create(unsigned int flags)
 	a->planned_only = pl && pl[0] == '1';
 	if (const char *zm = getenv("PECH_ASYNC_ZC_MAX"))
 		a->zc_max = (size_t)strtoull(zm, nullptr, 0);
+	if (const char *ms = getenv("PECH_ASYNC_SLOTS")) {
+		const unsigned v = (unsigned)strtoul(ms, nullptr, 0);
+		a->max_slots = v >= 1u && v <= kMaxSlots ? v : kMaxSlots;
+	}
 	if (hipGetDevice(&a->dev) != hipSuccess) {
 		pech_internal_set_err("crc32c_async_create: %s", hipGetErrorString(hipGetLastError()));
 		crc32c_async_destroy(a);
