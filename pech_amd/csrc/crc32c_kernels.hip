@@ -1519,7 +1519,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// full blocks: every lane's rows valid, prefetch stays inside every run
 		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
 			const uint64_t base = S.ad + (uint64_t)blk * U * rsb;
-#ifdef PECH_STAMPS
+#if defined(PECH_STAMPS) && !defined(PECH_STAMP_FIN)
 			if (nstep == 0 && (blk == nblk / 4u || blk == nblk / 2u || blk == 3u * nblk / 4u))
 				tq[blk == nblk / 4u ? 0 : (blk == nblk / 2u ? 1 : 2)] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1580,6 +1580,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// already fetch the next step's first rows
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S), rsb), 4);
+#ifdef PECH_STAMP_FIN // stamps build: time spent planning steps inside the loop (sum, 25 % stamp slot)
+		const uint64_t t_pl0 = __builtin_amdgcn_s_memrealtime();
+#endif
 		uint32_t npos = S.pos, nlr = S.lr, nrem = S.rem;
 		if (jmax > 1u && nrem == 0) {
 			// item done: the next one from the pool (wave-uniform branch,
@@ -1630,6 +1633,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				  : plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
 #endif
 		const uint32_t tpow_n = COPY ? 0u : rowpow(consts, N); // (used when N ends)
+#ifdef PECH_STAMP_FIN
+		tq[0] += __builtin_amdgcn_s_memrealtime() - t_pl0;
+#endif
 		if constexpr (COPY) { // block discipline: this block's rows and stores, then the next step's loads
 			const bool more = N.T != 0;
 			const Step &L = more ? N : S;

@@ -75,6 +75,8 @@ if os.environ.get("PECH_STAMP_FIN") == "1":  # stamps built with -DPECH_STAMP_FI
     print("last step's fold+shift us p10/p50/p90/max: %.2f %.2f %.2f %.2f" % (pct(fin, 10), pct(fin, 50), pct(fin, 90), fin.max()))
     print("after it (deferral flush) us p50/p90/max: %.2f %.2f %.2f" % (pct(flush, 50), pct(flush, 90), flush.max()))
     print("start->last fold us p10/p50/p90/max: %.1f %.1f %.1f %.1f" % tuple(x / 100 for x in (pct(q3 - s, 10), pct(q3 - s, 50), pct(q3 - s, 90), (q3 - s).max())))
+    plan = (q1 + t0) / 100  # (a sum of durations, not a time stamp: undo the shift)
+    print("steps planned in the loop, us per wave p10/p50/p90/max: %.2f %.2f %.2f %.2f" % (pct(plan, 10), pct(plan, 50), pct(plan, 90), plan.max()))
 hist, edges = np.histogram(e / 100, bins=12)
 print("end-time histogram (us):", [(round(float(edges[i]),1), int(hist[i])) for i in range(len(hist))])
 
