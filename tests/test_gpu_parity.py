@@ -252,6 +252,28 @@ def test_single_huge_buffer_split_over_all_groups(torch_dev, P):
         assert int(got[0]) == O.crc(seed, host[off:off + L])
 
 
+def test_near_4gib_buffer(torch_dev, P):
+    """One buffer of 2^32 - 100 bytes, unaligned: its split runs end up to 2^25
+    rows before the buffer's end, past the row-power table's 2^18 rows (the
+    digits above it, v0.25) and at the rows-after bit 25.  The
+    check is the SSE4.2 oracle (cross-checked against the compiled reference in
+    test_oracle.py), or the byte loop without SSE4.2."""
+    torch, dev = torch_dev
+    L = (1 << 32) - 100
+    blk = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device=dev)
+    buf = torch.empty(64 * (64 << 20) + 64, dtype=torch.uint8, device=dev)
+    body = buf[:64 * (64 << 20)].view(64, -1)
+    body.copy_(blk.expand(64, -1))
+    body += torch.arange(64, dtype=torch.uint8, device=dev).view(64, 1)  # (uint8 wraps)
+    buf[64 * (64 << 20):] = 7
+    host = buf.cpu().numpy()
+    H = O.hw()
+    ref = (lambda s, a: H.hw_crc32c(s, a.ctypes.data, a.nbytes)) if H else O.crc
+    for off, seed in ((3, 0x9E3779B9), (0, 0)):
+        got = dev_crcs(torch, P, buf, [off], [L], [seed])
+        assert int(got[0]) == ref(seed, host[off:off + L]), (off, seed)
+
+
 def test_sensitivity_constant_data(torch_dev, P):
     torch, dev = torch_dev
     for val in (0x00, 0xFF):
