@@ -78,10 +78,14 @@ typedef void (*crc32c_done_fn)(void *arg, uint32_t crc, int err);
 /* The default since round 4; accepted for callers written before. */
 #define CRC32C_ASYNC_ZEROCOPY 1u
 /* crc32c_pages payloads from 32 KiB up are DMA'd to device staging instead:
- * more host-link bandwidth for large payloads (MI355X: 42-50 against 36-37
- * GiB/s at 1-4 MiB) for more of the caller's CPU.  The copies are recorded
- * at submit and issued together when the slot launches (one batched call
- * where the HIP runtime has hipMemcpyBatchAsync).  Not with ZEROCOPY. */
+ * more host-link bandwidth for large payloads (MI355X: 42 against 36 GiB/s
+ * at 4 MiB, for 5 against 4 us of the caller's CPU per payload; but 5
+ * against 19 GiB/s at 64 KiB).  The copies are recorded at
+ * submit and issued together when the slot launches (one batched call where
+ * the HIP runtime has hipMemcpyBatchAsync).  One slot's copies are in flight
+ * at a time: a filled slot waits, without a HIP call, and launches from
+ * crc32c_async_complete() (or a wait for a free slot, or drain) once the
+ * slots before it are harvested.  Not with ZEROCOPY. */
 #define CRC32C_ASYNC_DMA 2u
 
 /* A context on the current device: its own HIP stream, staging slots and
