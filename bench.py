@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """bench.py -- CRC32C GiB/s on device-resident object buffers (BASELINE.json).
 
-One "step" = one pass of the hot path (plan + main kernel of
-libpech_crc32c.so) over one batch of device-resident synthetic buffers.
+One "step" = one pass of the hot path (libpech_crc32c.so's kernels: one
+flat launch for batches of up to 256 buffers, plan + main beyond) over one
+batch of device-resident synthetic buffers.
 Default workload = BASELINE config 3 / per-GPU shard of config 5:
 256 x 4 MiB buffers (1 GiB) per GPU, rotating between 2 distinct batches
 (2 GiB resident) so the 256 MiB Infinity Cache cannot serve a step.
@@ -90,6 +91,9 @@ def parse():
                     help="device entry point: planned = crc32c_dev_batch_ws_async (plan + main kernel), small = "
                          "crc32c_dev_batch_small_async (direct kernel, one launch); auto = small when every buffer "
                          "is below 32 KiB, as the async layer routes its slots")
+    ap.add_argument("--flat-max", type=int, default=256,
+                    help="device batches of at most this many buffers run as one launch with no plan kernel "
+                         "(crc32c_set_flat_max; 0 = always plan + main, the A/B against the planned path)")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no HIP events around the main kernel (roofline unavailable)")
     ap.add_argument("--data", choices=["random", "zeros", "ones"], default="random",
@@ -150,6 +154,7 @@ def main():
     import pech_amd as P
     from pech_amd import _lib
 
+    P.set_flat_max(args.flat_max)
     sizes, rotate, desc = CONFIGS[args.config]
     if args.rotate:
         rotate = args.rotate
@@ -162,6 +167,7 @@ def main():
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     maxs = max(1, args.streams)
     small_api = args.api == "small" or (args.api == "auto" and int(sizes.max()) < (32 << 10))
+    flat = not small_api and args.op == "crc" and n <= min(args.flat_max, 256)
 
     class Shard:
         """One device's batches: `rotate` distinct resident batches of random
@@ -332,7 +338,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": ("pech_crc32c_direct_copy" if dsts else "pech_crc32c_direct") if small_api else
-                               ("pech_crc32c_main_copy" if dsts else "pech_crc32c_main"),
+                               "pech_crc32c_flat" if flat else ("pech_crc32c_main_copy" if dsts else "pech_crc32c_main"),
                      "bytes_per_launch": algo_bytes, "avg_launch_us": round(avg_kernel_s * 1e6, 2),
                      "launch_us_p10_p50_p90": [round(float(np.percentile(samples, q)), 2) for q in (10, 50, 90)]
                      if len(samples) else None,

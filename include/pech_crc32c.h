@@ -140,6 +140,14 @@ int crc32c_dev_copy_batch_ws_async(const struct crc32c_desc *d_descs, const uint
 int crc32c_dev_copy_batch_small_async(const struct crc32c_desc *d_descs, const uint64_t *d_dsts, uint32_t *d_out,
 				      unsigned int n, void *stream);
 
+/* Device batches (crc32c_dev_batch_async / _ws_async, and the batches the
+ * synchronous and async host paths launch) of at most n buffers run as ONE
+ * kernel launch with no plan kernel; larger ones, fused copies and batches
+ * captured in a graph take the two-launch plan + main path.  Default and
+ * maximum 256; 0 = always plan + main.  Results are identical either way.
+ * Returns the previous value. */
+unsigned int crc32c_set_flat_max(unsigned int n);
+
 /* Pre-size the internal workspace of the current device for n buffers. */
 int crc32c_dev_reserve(unsigned int n);
 

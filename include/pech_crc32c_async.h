@@ -95,6 +95,16 @@ typedef void (*crc32c_done_fn)(void *arg, uint32_t crc, int err);
  * collective). */
 struct crc32c_async *crc32c_async_create(unsigned int flags);
 
+/* The same on GPU `device` (the caller's current device is left as it was). */
+struct crc32c_async *crc32c_async_create_on(int device, unsigned int flags);
+
+/* The GPUs a caller that spreads its payloads over several contexts should
+ * use, one context each: every visible device, or the PECH_DEVICES list
+ * ("0,0" repeats a device: two contexts on one GPU, how a one-GPU machine
+ * rehearses a node).  Fills up to max entries of devs; returns the count, or
+ * a negative errno (-ENODEV: no GPU, -EINVAL: a bad list). */
+int crc32c_async_devices(int *devs, int max);
+
 /* The eventfd (EFD_NONBLOCK | EFD_CLOEXEC): readable while finished batches
  * wait for crc32c_async_complete().  Owned by the context. */
 int crc32c_async_fd(const struct crc32c_async *a);
@@ -128,6 +138,16 @@ unsigned int crc32c_async_pending(const struct crc32c_async *a);
 
 /* Drain, then free the context (its eventfd is closed). */
 void crc32c_async_destroy(struct crc32c_async *a);
+
+/* Per-context counters (no HIP call). */
+struct crc32c_async_stats {
+	int device;             /* the GPU the context runs on                    */
+	uint64_t submitted;     /* accepted submissions                           */
+	uint64_t launches;      /* batches launched                               */
+	unsigned int inflight;  /* batches launched and not yet harvested         */
+	unsigned int queued;    /* CRC32C_ASYNC_DMA: filled slots waiting to launch */
+};
+int crc32c_async_get_stats(const struct crc32c_async *a, struct crc32c_async_stats *st);
 
 /* ---- CRC reuse by concatenation (host algebra, no data pass) ----------- */
 /* crc32c(seed, S_0 || S_1 || ... || S_{n-1}) from the segments' zero-seeded

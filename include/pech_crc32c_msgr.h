@@ -81,6 +81,11 @@ void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c);
  * free the adapter. */
 void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c);
 
+/* The async context the connection submits to (NULL for NULL): a messenger
+ * with one context per GPU flushes and completes only its connection's
+ * after each pass of con_work. */
+struct crc32c_async *crc32c_msgr_conn_async(const struct crc32c_msgr_conn *c);
+
 /* Payloads of at most `bytes` (default 8 KiB, or PECH_CRC32C_MSGR_HOST_MAX
  * in the environment) are checksummed at once on the host instead of the
  * GPU: below the crossover the host routine costs less CPU time than the

@@ -29,6 +29,12 @@ class CStats(ctypes.Structure):
                 ("gpu_bytes", ctypes.c_uint64), ("gpu_fallbacks", ctypes.c_uint64)]
 
 
+class CAsyncStats(ctypes.Structure):
+    """struct crc32c_async_stats (include/pech_crc32c_async.h)."""
+    _fields_ = [("device", ctypes.c_int), ("submitted", ctypes.c_uint64), ("launches", ctypes.c_uint64),
+                ("inflight", ctypes.c_uint), ("queued", ctypes.c_uint)]
+
+
 # completion callback of include/pech_crc32c_async.h: (arg, crc, err)
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int)
 
@@ -56,6 +62,7 @@ SIGNATURES = {
     "crc32c_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     "crc32c_device_init": (ctypes.c_int, []),
     "crc32c_set_cpu_max": (ctypes.c_uint, [ctypes.c_uint]),
+    "crc32c_set_flat_max": (ctypes.c_uint, [ctypes.c_uint]),
     "crc32c_get_stats": (ctypes.c_int, [ctypes.c_void_p]),
     "crc32c_timing": (ctypes.c_int, [ctypes.c_int]),
     "crc32c_timing_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
@@ -67,6 +74,10 @@ SIGNATURES = {
     "crc32c_pages_is_pinned": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     "crc32c_pages_trim": (None, []),
     "crc32c_async_create": (ctypes.c_void_p, [ctypes.c_uint]),
+    "crc32c_async_create_on": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_uint]),
+    "crc32c_msgr_conn_async": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "crc32c_async_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "crc32c_async_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "crc32c_async_fd": (ctypes.c_int, [ctypes.c_void_p]),
     "crc32c_async_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint32,
                                            DONE_FN, ctypes.c_void_p]),

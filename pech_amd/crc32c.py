@@ -18,7 +18,7 @@ from ._lib import CDesc, Crc32cError, check, lib
 __all__ = [
     "crc32c", "crc32c_batch", "crc32c_shift", "crc32c_combine", "make_descs", "dev_batch_async",
     "dev_batch_small_async", "dev_batch_ws_async", "dev_copy_batch_ws_async", "workspace_bytes", "crc32c_tensors", "shard_ranges", "Crc32cError", "timing",
-    "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc", "set_cpu_max", "stats",
+    "timing_read", "timing_samples", "version", "crc32c_concat", "Pages", "AsyncCrc", "async_devices", "set_cpu_max", "set_flat_max", "stats",
 ]
 
 F_HOST, F_DEVICE, F_PINNED, F_ALL_DEVICES = 0, 1, 2, 4
@@ -38,6 +38,13 @@ def set_cpu_max(nbytes):
     """Drop-in routing: crc32c() calls of at most nbytes run on the host CPU
     (0: every non-empty call on the GPU).  Returns the previous value."""
     return int(lib().crc32c_set_cpu_max(int(nbytes)))
+
+
+def set_flat_max(n):
+    """Device batches of at most n buffers run as one launch with no plan
+    kernel (pech_crc32c_flat; default and maximum 256, 0 = always plan +
+    main).  Returns the previous value."""
+    return int(lib().crc32c_set_flat_max(int(n)))
 
 
 def stats():
@@ -265,16 +272,35 @@ class Pages:
             self.view = None
 
 
+def async_devices():
+    """crc32c_async_devices: the GPUs to spread async contexts over (every
+    visible device, or the PECH_DEVICES list)."""
+    devs = (ctypes.c_int * 64)()
+    n = lib().crc32c_async_devices(devs, 64)
+    check(n if n < 0 else 0, "crc32c_async_devices")
+    return list(devs[:n])
+
+
 class AsyncCrc:
     """crc32c_async context (include/pech_crc32c_async.h): submit host
     payloads, poll fd() from an event loop, complete() runs the callbacks."""
 
-    def __init__(self, dma=False):
+    def __init__(self, dma=False, zerocopy=None, device=None):
         """dma=False: crc32c_pages payloads are read in place (the default);
-        dma=True: CRC32C_ASYNC_DMA, DMA'd to device staging at launch."""
+        dma=True: CRC32C_ASYNC_DMA, DMA'd to device staging at launch.
+        zerocopy: the round-3 keyword, kept as an alias (zerocopy=True is the
+        default mode, CRC32C_ASYNC_ZEROCOPY; zerocopy=False asks for DMA);
+        zerocopy=True together with dma=True is refused, as
+        crc32c_async_create refuses both flags.  device: the GPU
+        (crc32c_async_create_on), default the current one."""
         from ._lib import DONE_FN
 
-        self._h = lib().crc32c_async_create(2 if dma else 0)
+        if zerocopy is not None:
+            if zerocopy and dma:
+                raise ValueError("AsyncCrc: zerocopy=True and dma=True are exclusive")
+            dma = dma or not zerocopy
+        flags = 2 if dma else (1 if zerocopy else 0)
+        self._h = lib().crc32c_async_create(flags) if device is None else lib().crc32c_async_create_on(device, flags)
         if not self._h:
             raise Crc32cError(f"crc32c_async_create failed: {lib().crc32c_last_error().decode()}")
         self._keep = {}  # submission key -> (payload ref, python callback)
@@ -293,6 +319,15 @@ class AsyncCrc:
     @property
     def handle(self):
         return self._h
+
+    def stats(self):
+        """crc32c_async_get_stats as a dict (device, submitted, launches,
+        inflight, queued)."""
+        from ._lib import CAsyncStats
+
+        st = CAsyncStats()
+        check(lib().crc32c_async_get_stats(self._h, ctypes.byref(st)), "crc32c_async_get_stats")
+        return {name: int(getattr(st, name)) for name, _ in CAsyncStats._fields_}
 
     def fd(self):
         return lib().crc32c_async_fd(self._h)

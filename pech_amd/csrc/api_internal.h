@@ -15,6 +15,10 @@
 // workspace (pech_ws_bytes(n) bytes, 256-byte aligned); current device
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
 				     size_t ws_bytes, hipStream_t stream, bool small = false);
+// The GPUs a multi-device caller spreads over: PECH_DEVICES="0,0,..." (a
+// repeated id puts several shards or contexts on one GPU: how one-GPU boxes
+// rehearse eight) or every visible device.  Count, or a negative errno.
+PECH_HIDDEN int pech_internal_device_list(int *devs, int max, int max_per_dev);
 // set the thread's crc32c_last_error() text
 PECH_HIDDEN void pech_internal_set_err(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 

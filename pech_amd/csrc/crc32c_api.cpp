@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -41,6 +42,8 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *, uint32_t, const uint
 					 hipStream_t, hipEvent_t, hipEvent_t, const uint64_t *);
 extern "C" hipError_t pech_launch_small(const void *, uint32_t, uint32_t, const uint32_t *, uint32_t *, uint32_t,
 					hipStream_t);
+extern "C" hipError_t pech_launch_flat(const pech_desc *, uint32_t, const uint32_t *, uint32_t *, uint32_t, uint32_t,
+				       uint64_t *, uint64_t, hipStream_t, hipEvent_t, hipEvent_t);
 
 // ---------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -259,6 +262,35 @@ static bool capturing(hipStream_t s)
 	return st != hipStreamCaptureStatusNone;
 }
 
+// Batches of at most g_flat_max buffers run as ONE launch (pech_crc32c_flat:
+// no plan kernel) -- C3's 256 x 4 MiB, the async layer's slots of large
+// payloads, a single large message.  Its workgroup 0 publishes the zeroed
+// out[] through the first 8 bytes of the workspace and a tag that must differ
+// from every earlier launch's on that workspace: a process-wide 64-bit
+// counter from a per-process start, so a tag left in recycled memory by
+// another run does not match either.  A graph replays its captured tag, so
+// captured batches take plan + main.
+static std::atomic<unsigned int> g_flat_max{PECH_FLAT_MAX};
+static std::atomic<uint64_t> g_flat_tag{0};
+static std::once_flag g_flat_tag_init;
+
+static uint64_t flat_tag()
+{
+	std::call_once(g_flat_tag_init, [] {
+		uint64_t t = 0;
+		FILE *f = fopen("/dev/urandom", "rb");
+		if (!f || fread(&t, sizeof(t), 1, f) != 1)
+			t = (uint64_t)(uintptr_t)&t ^ ((uint64_t)clock() << 32) ^ 0x9E3779B97F4A7C15ull;
+		if (f)
+			fclose(f);
+		g_flat_tag.store(t);
+	});
+	uint64_t t;
+	while ((t = g_flat_tag.fetch_add(1) + 1) == 0) // (0: a zeroed workspace's value)
+		;
+	return t;
+}
+
 // d_dsts != NULL: fused CRC + copy (d_dsts[i] receives descriptor i's bytes)
 static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
 			size_t ws_bytes, hipStream_t stream, const uint64_t *d_dsts = nullptr)
@@ -275,9 +307,11 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			set_err("workspace must be 256-byte aligned");
 			return -EINVAL;
 		}
+		const bool flat = !d_dsts && m <= g_flat_max.load(std::memory_order_relaxed) && !capturing(stream);
 		const pech_ws w = pech_ws_carve(ws, m);
-		HIP_TRY(pech_launch_plan(d_descs + off, m, &w, c->d_consts, d_out + off, d_dsts ? d_dsts + off : nullptr,
-					 stream));
+		if (!flat)
+			HIP_TRY(pech_launch_plan(d_descs + off, m, &w, c->d_consts, d_out + off,
+						 d_dsts ? d_dsts + off : nullptr, stream));
 		TimedLaunch tl{};
 		if (g_timing) {
 			if (!c->free_events.empty()) {
@@ -288,8 +322,12 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 				HIP_TRY(hipEventCreate(&tl.b));
 			}
 		}
-		HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN, d_dsts != nullptr,
-					 stream, tl.a, tl.b));
+		if (flat)
+			HIP_TRY(pech_launch_flat(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN,
+						 (uint64_t *)ws, flat_tag(), stream, tl.a, tl.b));
+		else
+			HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN,
+						 d_dsts != nullptr, stream, tl.a, tl.b));
 		if (g_timing)
 			c->pending.push_back(tl);
 	}
@@ -361,6 +399,41 @@ PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, 
 	if (rc)
 		return rc;
 	return small ? launch_small(c, d_descs, d_out, n, stream) : launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream);
+}
+
+PECH_HIDDEN int pech_internal_device_list(int *devs, int max, int max_per_dev)
+{
+	int nd = 0;
+	if (const char *e = getenv("PECH_DEVICES")) {
+		for (const char *p = e; *p && nd < max;) {
+			char *q = nullptr;
+			const long v = strtol(p, &q, 10);
+			if (q == p)
+				break;
+			devs[nd++] = (int)v;
+			p = *q == ',' ? q + 1 : q;
+		}
+	} else {
+		HIP_TRY(hipGetDeviceCount(&nd));
+		nd = nd < max ? nd : max;
+		for (int d = 0; d < nd; ++d)
+			devs[d] = d;
+	}
+	int ndev_all = 0;
+	HIP_TRY(hipGetDeviceCount(&ndev_all));
+	int used[64] = {0};
+	for (int k = 0; k < nd; ++k) {
+		if (devs[k] < 0 || devs[k] >= ndev_all || devs[k] >= 64 || used[devs[k]] >= max_per_dev) {
+			set_err("bad device list (PECH_DEVICES)");
+			return -EINVAL;
+		}
+		used[devs[k]]++;
+	}
+	if (nd == 0) {
+		set_err("no usable GPU");
+		return -ENODEV;
+	}
+	return nd;
 }
 
 PECH_HIDDEN void pech_internal_set_err(const char *fmt, ...)
@@ -535,36 +608,10 @@ static int shard_pinned(const void *const *bufs, const unsigned int *lens, const
 static int multi_device_pinned(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds,
 			       uint32_t *out, unsigned int n)
 {
-	int devs[64], nd = 0;
-	if (const char *e = getenv("PECH_DEVICES")) {
-		for (const char *p = e; *p && nd < 64;) {
-			char *q = nullptr;
-			const long v = strtol(p, &q, 10);
-			if (q == p)
-				break;
-			devs[nd++] = (int)v;
-			p = *q == ',' ? q + 1 : q;
-		}
-	} else {
-		HIP_TRY(hipGetDeviceCount(&nd));
-		nd = nd < 64 ? nd : 64;
-		for (int d = 0; d < nd; ++d)
-			devs[d] = d;
-	}
-	int ndev_all = 0;
-	HIP_TRY(hipGetDeviceCount(&ndev_all));
-	int used[64] = {0};
-	for (int k = 0; k < nd; ++k) {
-		if (devs[k] < 0 || devs[k] >= ndev_all || devs[k] >= 64 || used[devs[k]] >= PECH_MAX_SHARDS_PER_DEV) {
-			set_err("crc32c_batch: bad device list (PECH_DEVICES)");
-			return -EINVAL;
-		}
-		used[devs[k]]++;
-	}
-	if (nd == 0) {
-		set_err("no usable GPU");
-		return -ENODEV;
-	}
+	int devs[64];
+	const int nd = pech_internal_device_list(devs, 64, PECH_MAX_SHARDS_PER_DEV);
+	if (nd < 0)
+		return nd;
 	uint64_t total = 0;
 	for (unsigned int i = 0; i < n; ++i)
 		total += lens[i];
@@ -917,6 +964,11 @@ unsigned int crc32c_set_cpu_max(unsigned int bytes)
 {
 	(void)cpu_max(); // the environment is read first, so this call wins
 	return g_cpu_max.exchange(bytes);
+}
+
+unsigned int crc32c_set_flat_max(unsigned int n)
+{
+	return g_flat_max.exchange(n < PECH_FLAT_MAX ? n : PECH_FLAT_MAX);
 }
 
 int crc32c_get_stats(struct crc32c_stats *st)

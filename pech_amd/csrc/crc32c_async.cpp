@@ -334,7 +334,8 @@ struct crc32c_async {
 	// destroy (where a DMA-mode thread's time goes; measurement only)
 	bool prof = false;
 	uint64_t prof_ns[5] = {0, 0, 0, 0, 0}; // copies issued, kernels + D2H + host function, waits for a slot, submit, complete
-	uint64_t prof_launches = 0;
+	uint64_t launches = 0;  // batches launched (crc32c_async_get_stats)
+	uint64_t submitted = 0; // submissions accepted
 };
 
 static inline uint64_t thread_ns()
@@ -527,8 +528,15 @@ static int reap(crc32c_async *a, bool wait_oldest, DeviceGuard *dg = nullptr)
 		}
 		a->inflight.pop_front();
 		harvest(a, s, err);
-		if (wait_oldest)
+		if (wait_oldest) {
+			// CRC32C_ASYNC_DMA: the next slot in line waited for this one;
+			// it launches now, so the copy engine and the GPU work while the
+			// caller fills the slot it waited for (it used to wait
+			// for the next complete() or blocking get_slot)
+			if (!err && !a->err && !a->inflight.empty() && a->inflight.front()->queued && (!dg || dg->ensure()))
+				(void)issue_slot(a, a->inflight.front()); // (a failure is sticky in a->err)
 			return err;
+		}
 	}
 	return 0;
 }
@@ -601,10 +609,11 @@ static int fail_slot(crc32c_async *a, Slot *s, int err)
 static int issue_slot(crc32c_async *a, Slot *s)
 {
 	const unsigned m = (unsigned)s->pieces.size();
-	a->prof_launches++;
+	a->launches++;
 	ProfScope ps_copies(a, 0);
 	if (!s->dma.empty()) {
 		hipError_t e = hipErrorInvalidValue;
+		size_t from = 0; // first copy the per-copy fallback issues
 		if (!pech_fault(PECH_FAULT_ASYNC_DMA)) {
 			e = hipErrorNotSupported;
 			if (batch_copy_fn bc = batch_copy()) {
@@ -615,17 +624,32 @@ static int issue_slot(crc32c_async *a, Slot *s)
 					srcs.push_back(c.src);
 					sizes.push_back(c.bytes);
 				}
-				size_t fail_idx = 0;
+				size_t fail_idx = SIZE_MAX;
 				e = bc(dsts.data(), srcs.data(), sizes.data(), dsts.size(), nullptr, nullptr, 0, &fail_idx,
 				       s->stream);
+				// copies before fail_idx are queued: the per-copy calls resume
+				// there, so none is issued twice
+				if (e != hipSuccess && fail_idx < s->dma.size())
+					from = fail_idx;
+				if (e != hipSuccess && e != hipErrorNotSupported && e != hipErrorInvalidValue) {
+					static std::once_flag warned;
+					const hipError_t e0 = e;
+					std::call_once(warned, [&] {
+						fprintf(stderr, "pech_crc32c: hipMemcpyBatchAsync failed at copy %zu: %s; "
+								"issuing the rest one call each\n",
+							from, hipGetErrorString(e0));
+					});
+				}
 			}
 			if (e != hipSuccess) { // no batched call in this runtime (or it refused): one call each
 				(void)hipGetLastError();
 				e = hipSuccess;
-				for (const DmaCopy &c : s->dma)
+				for (size_t k = from; k < s->dma.size(); ++k) {
+					const DmaCopy &c = s->dma[k];
 					if ((e = hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyHostToDevice, s->stream)) !=
 					    hipSuccess)
 						break;
+				}
 			}
 		}
 		if (e != hipSuccess) {
@@ -738,6 +762,51 @@ extern "C" struct crc32c_async *crc32c_async_create(unsigned int flags)
 	return a;
 }
 
+extern "C" struct crc32c_async *crc32c_async_create_on(int device, unsigned int flags)
+{
+	struct crc32c_async *a = nullptr;
+	on_lib_stack([&] {
+		int ndev = 0;
+		if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+			(void)hipGetLastError();
+			pech_internal_set_err("crc32c_async_create_on: no device %d", device);
+			return 0;
+		}
+		DeviceGuard dg(device);
+		if (!dg.ok) {
+			pech_internal_set_err("crc32c_async_create_on: cannot select device %d", device);
+			return 0;
+		}
+		a = async_create(flags);
+		return 0;
+	});
+	return a;
+}
+
+extern "C" int crc32c_async_devices(int *devs, int max)
+{
+	if (!devs || max <= 0) {
+		pech_internal_set_err("crc32c_async_devices: invalid arguments");
+		return -EINVAL;
+	}
+	return on_lib_stack([&] { return pech_internal_device_list(devs, max < 64 ? max : 64, 16); });
+}
+
+extern "C" int crc32c_async_get_stats(const struct crc32c_async *a, struct crc32c_async_stats *st)
+{
+	if (!a || !st) {
+		pech_internal_set_err("crc32c_async_get_stats: invalid arguments");
+		return -EINVAL;
+	}
+	st->device = a->dev;
+	st->submitted = a->submitted;
+	st->launches = a->launches;
+	st->inflight = st->queued = 0;
+	for (const Slot *s : a->inflight)
+		(s->queued ? st->queued : st->inflight)++;
+	return 0;
+}
+
 extern "C" int crc32c_async_fd(const struct crc32c_async *a)
 {
 	return a ? a->efd : -EINVAL;
@@ -818,6 +887,7 @@ static int async_submit(struct crc32c_async *a, const void *buf, unsigned int le
 	Item &it = a->items[id - a->base];
 	it.placed = true;
 	it.total = placed;
+	a->submitted++;
 	Slot *s = a->cur;
 	if (s && (s->pieces.size() == kSlotDescs || s->used >= kSlotBytes || s->zc_bytes >= kSlotBytes)) {
 		const int rc = launch_slot(a);
@@ -909,6 +979,8 @@ extern "C" int crc32c_async_drain(struct crc32c_async *a)
 			if (r && !r0)
 				r0 = r;
 		}
+		if (!r0)
+			r0 = a->err; // (e.g. a queued slot that reap() launched and that failed)
 		uint64_t cnt;
 		while (read(a->efd, &cnt, sizeof(cnt)) > 0) {
 		}
@@ -939,7 +1011,7 @@ extern "C" void crc32c_async_destroy(struct crc32c_async *a)
 		fprintf(stderr,
 			"{\"async_prof\": {\"launches\": %llu, \"thread_cpu_us\": {\"copies\": %.1f, \"launch\": %.1f, "
 			"\"slot_wait\": %.1f, \"submit\": %.1f, \"complete\": %.1f}}}\n",
-			(unsigned long long)a->prof_launches, a->prof_ns[0] / 1e3, a->prof_ns[1] / 1e3, a->prof_ns[2] / 1e3,
+			(unsigned long long)a->launches, a->prof_ns[0] / 1e3, a->prof_ns[1] / 1e3, a->prof_ns[2] / 1e3,
 			a->prof_ns[3] / 1e3, a->prof_ns[4] / 1e3);
 	if (a->efd >= 0)
 		close(a->efd);

@@ -609,17 +609,63 @@ __device__ __forceinline__ pech_core load_spec(const pech_core *__restrict__ cor
 	return c;
 }
 
+// ---- flat batches (pech_crc32c_flat): n <= PECH_FLAT_MAX, no plan kernel ----
+// Every wave reads the batch's descriptors itself and keeps them in LDS as
+// {addr, rows, meta} per position, in descriptor order (L_FLAT, the chunk
+// table's space: a flat launch has no chunks).  rows are the 128-byte lines
+// holding ALL of the buffer's bytes, as in the direct kernel: no tail block
+// and no plan kernel.  meta = position | T << 20, with T (0..127) the zero
+// bytes after the buffer in its last line.  A run that ends its buffer keeps
+// kb bytes of each lane's piece of that line (Step.oz bits 12-16; the
+// position then has 12 bits) and is multiplied by x^(-8 T) at its end:
+// m = 128 ra - T.
+#define L_FLAT L_NZ
+#define PECH_FLAT_T(meta) (((meta) >> 20) & 127u)
+#define PECH_FLAT_KB_SHIFT 12u
+static_assert(PECH_FLAT_MAX * 16u <= 4096u && PECH_FLAT_MAX <= 4096u, "flat table: 16 B per position in L_NZ, 12-bit positions");
+
+__device__ __forceinline__ pech_core flat_core(const uint32_t *lds, uint32_t p)
+{
+	const u32x4 v = *(const u32x4 *)(lds + L_FLAT / 4u + 4u * p);
+	pech_core c;
+	c.addr = ((uint64_t)v.y << 32) | v.x;
+	c.rows = v.z;
+	c.meta = v.w;
+	return c;
+}
+
+// Step.oz bits of lane g8 for a run that ends its buffer (last): the zl flag
+// and the bytes kb of the lane's last-line piece that are the buffer's
+template <bool FLAT>
+__device__ __forceinline__ uint32_t tail_of(bool last, uint32_t g8, uint32_t meta)
+{
+	if (!FLAT)
+		return tail_bits(last, g8, PECH_META_ZT(meta));
+	const uint32_t e = 128u - PECH_FLAT_T(meta), lo = 16u * g8;
+	const uint32_t kb = e > lo ? min(e - lo, 16u) : 0u;
+	return last ? (1u << 27) | (kb << PECH_FLAT_KB_SHIFT) : 0u;
+}
+
+template <bool FLAT>
+__device__ __forceinline__ uint32_t mp_of(uint32_t ra, uint32_t meta)
+{
+	return FLAT ? (ra << 7) | PECH_FLAT_T(meta) : mp_bits(ra, meta);
+}
+
 // Work out the wave's next step from its cursor (pos, lr, rem).  COPY: also
 // the destination offset of each group's buffer (deltas[orig], scalar loads).
 // PRE: `spec` holds cores[ppos + grp] (loaded at kernel entry); a step that
 // starts at ppos takes its descriptors from it instead of loading them.
 // grid: static shares, whose small-buffer steps lie on a grid of 8 positions.
-template <bool COPY, bool PRE = false>
+// FLAT: the descriptors come from the wave's LDS table (flat_core) for
+// positions < nflat, empty buffers included (skipped here).
+template <bool COPY, bool PRE = false, bool FLAT = false>
 __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
 					  const uint32_t *lds, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
 					  uint32_t g8, uint32_t grp, bool grid, const pech_core &spec = pech_core{},
-					  uint32_t ppos = 0)
+					  uint32_t ppos = 0, uint32_t nflat = 0)
 {
+	static_assert(!(FLAT && (COPY || PRE)), "flat batches: CRC only, descriptors from LDS");
 	Step S;
 	int64_t dl = 0;
 	S.T = 0;
@@ -635,15 +681,29 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 	for (;;) {
 		if (rem == 0)
 			break;
-		const uint32_t c = pos >> 10;
-		const uint32_t nzc = uni(lds[L_NZ / 4u + c]);
-		if ((pos & 1023u) >= nzc) {
-			pos = (c + 1u) << 10;
-			continue;
+		uint32_t c, nzc;
+		if (FLAT) {
+			if (pos >= nflat) { // (never while rows remain)
+#ifdef PECH_DEBUG_BOUNDS
+				printf("PECH OOB flat cursor pos %u n %u rem %u\n", pos, nflat, rem);
+#endif
+				break;
+			}
+			c = 0;
+			nzc = nflat;
+		} else {
+			c = pos >> 10;
+			nzc = uni(lds[L_NZ / 4u + c]);
+			if ((pos & 1023u) >= nzc) {
+				pos = (c + 1u) << 10;
+				continue;
+			}
 		}
 		const bool hit = PRE && pos == ppos; // wave-uniform
 		pech_core cd;
-		if (hit)
+		if (FLAT)
+			cd = flat_core(lds, pos);
+		else if (hit)
 			cd = spec; // lanes 0-7 (group 0) hold cores[pos]; uni() reads lane 0
 		else
 			cd = cores[pos];
@@ -652,11 +712,14 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			printf("PECH OOB preloaded descriptor pos %u grp %u\n", pos, grp);
 #endif
 		const uint32_t rows0 = uni(cd.rows);
+		if (FLAT && rows0 == 0u) { // an empty buffer (flat batches keep them in place; lr is 0 here)
+			++pos;
+			continue;
+		}
 		const uint64_t a0 = uni64(cd.addr);
 		const uint64_t vb0 = a0 & ~(uint64_t)(PECH_ROW_BYTES - 1u);
 		const uint32_t lb0 = (uint32_t)a0 & (PECH_ROW_BYTES - 1u);
 		const uint32_t meta0 = uni(cd.meta);
-		const uint32_t zt0 = PECH_META_ZT(meta0);
 		const uint32_t avail0 = rows0 - lr;
 		// A large buffer (or what is left of it) goes to 8 slices when at least
 		// 64 of its rows are to be walked: a remainder below PECH_SPLIT_ROWS
@@ -672,8 +735,8 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			S.nl = nn;
 			S.nu = nn;
 			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) | ra_bit(rows0 - st - nn) |
-			       tail_bits(st + nn == rows0, g8, zt0); // the first / this slice ends the buffer
-			S.mp = mp_bits(rows0 - st - nn, meta0);
+			       tail_of<FLAT>(st + nn == rows0, g8, meta0); // the first / this slice ends the buffer
+			S.mp = mp_of<FLAT>(rows0 - st - nn, meta0);
 			S.T = q + (rm ? 1u : 0u);
 			S.nmin = q;
 			if (COPY)
@@ -697,7 +760,13 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			// workspace memory); such entries are never used.
 			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
 			int64_t mdl = 0;
-			if (hit) {
+			if (FLAT) { // each group its own entry (LDS: no scalar-load selects)
+				const pech_core dj = flat_core(lds, min(pos + grp, nflat - 1u));
+				vlo = (uint32_t)dj.addr;
+				vhi = (uint32_t)(dj.addr >> 32);
+				mrows = dj.rows;
+				mmeta = dj.meta;
+			} else if (hit) {
 				vlo = (uint32_t)spec.addr;
 				vhi = (uint32_t)(spec.addr >> 32);
 				mrows = spec.rows;
@@ -730,7 +799,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			my.rows = mrows;
 			my.meta = mmeta;
 			const uint32_t myp = pos + grp;
-			const bool inchunk = (myp & 1023u) < nzc && (myp >> 10) == c;
+			const bool inchunk = FLAT ? myp < nflat : (myp & 1023u) < nzc && (myp >> 10) == c;
 			const uint32_t myrows = inchunk ? my.rows : 0u;
 			// cut at the first non-first group whose buffer is split or out of chunk
 			const bool cut = grp > 0 && (!inchunk || myrows >= PECH_SPLIT_ROWS);
@@ -762,12 +831,11 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			const uint32_t used = whole && !own ? rem : min(lane_value(incl, 63), rem);
 			const uint32_t mylb = (uint32_t)my.addr & (PECH_ROW_BYTES - 1u);
 			const uint64_t myvb = my.addr & ~(uint64_t)(PECH_ROW_BYTES - 1u);
-			const uint32_t myzt = PECH_META_ZT(my.meta);
 			if (nu) {
 				S.ad = myvb + (uint64_t)mylr * PECH_ROW_BYTES + 16u * g8;
 				S.nl = nu;
 				S.oz = PECH_META_ORIG(my.meta) | head_bits(mylr == 0, g8, mylb) | ra_bit(myrows - mylr - nu) |
-				       tail_bits(mylr + nu == myrows, g8, myzt); // the run ends the buffer
+				       tail_of<FLAT>(mylr + nu == myrows, g8, my.meta); // the run ends the buffer
 			} else {
 				// idle groups reload group 0's rows (valid memory: the redirect
 				// of row 0's pieces before the buffer kept), state ignored
@@ -777,7 +845,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			}
 			S.nu = nu;
 			dl = mdl;
-			S.mp = mp_bits(myrows - mylr - nu, my.meta);
+			S.mp = mp_of<FLAT>(myrows - mylr - nu, my.meta);
 #ifdef PECH_DEBUG_BOUNDS
 			const uint64_t bv = nu ? myvb : vb0;
 			S.blo = bv + 16u * ((nu ? mylb : lb0) >> 4);
@@ -886,6 +954,17 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 #define STEP_ZL(S) ((S).oz & (1u << 27)) // bit 28: STEP_SLOW (direct kernel), bit 29: PECH_OZ_RA25
 #define STEP_RA(S) ((uint64_t)((S).mp >> 7) | (uint64_t)((S).oz & PECH_OZ_RA25) >> 4) // rows after the run
 #define STEP_M(S) ((int64_t)(STEP_RA(S) * PECH_ROW_BYTES + ((S).mp & 15u)) - (int64_t)((S).mp & 0x70u))
+// flat batches: m = 128 ra - T, and the position in bits 0-11 (kb above it)
+template <bool FLAT>
+__device__ __forceinline__ int64_t step_m(const Step &S)
+{
+	return FLAT ? (int64_t)(STEP_RA(S) * PECH_ROW_BYTES) - (int64_t)(S.mp & 127u) : STEP_M(S);
+}
+template <bool FLAT>
+__device__ __forceinline__ uint32_t step_orig(const Step &S)
+{
+	return FLAT ? (S.oz & 0xFFFu) : STEP_ORIG(S);
+}
 // x^(8 * 128 * rows after the run), modulo the table's span (finish_run)
 __device__ __forceinline__ uint32_t rowpow(const uint32_t *consts, const Step &S)
 {
@@ -1003,9 +1082,13 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 
 // A trailing virtual piece (past the core's end, in the core's last row)
 // counts as zero; only the ragged and last blocks of a step can hold a run's
-// last row.
+// last row.  Flat batches: the lane keeps the first kb bytes of its piece of
+// the buffer's last line (the rest lies past the buffer).
+template <bool FLAT = false>
 __device__ __forceinline__ u32x4 zl_mask(const Step &S, uint32_t row, u32x4 v)
 {
+	if (FLAT)
+		return (STEP_ZL(S) && row == S.nu - 1u) ? keep_below(v, (S.oz >> PECH_FLAT_KB_SHIFT) & 31u) : v;
 	return (STEP_ZL(S) && row == S.nu - 1u) ? (u32x4)(0u) : v;
 }
 __device__ __forceinline__ bool zl_keep(const Step &S, uint32_t row)
@@ -1044,6 +1127,76 @@ struct Start {
 	uint64_t t_scan;
 #endif
 };
+
+// Every wave's equal share [r0, r1) of the batch's Rtot rows, the
+// workgroup's static rows [wg0, wg0 + wg_rows), the pool size (jmax) and the
+// rows the wave walks before pooling (rem_all); false when the whole
+// workgroup is idle (small batch).  (Shared by the planned and the flat
+// prologues.)
+template <bool COPY>
+__device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t rpw_min, uint32_t wave, bool uniform,
+					   bool il, Start &st)
+{
+	// Every wave gets an equal share of the batch's rows (at least rpw_min).
+	// Large batches: workgroup b gets rows [b Rtot / G, (b+1) Rtot / G) --
+	// proportional, not b * ceil(Rtot / W): the rounding drifted by up to a
+	// row per wave, a whole step of 8 small buffers after a few hundred
+	// waves, so some waves walked an extra step (2 -> 3 on unaligned
+	// 4,100-byte buffers) and set the launch's end.  Small batches: shares
+	// of rpw_min rows, the last workgroups idle.
+	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_min;
+	const uint32_t rpw = prop ? 0u : rpw_min;
+#ifdef PECH_FAST_DIV // A/B: 32-bit quotients when the products fit 32 bits (batches below 4 GiB / grid rows)
+	const uint64_t wg0 = prop ? div_u64_u32((uint64_t)blockIdx.x * Rtot, gridDim.x)
+				  : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+	const uint32_t wg_rows = prop ? (uint32_t)(div_u64_u32((uint64_t)(blockIdx.x + 1u) * Rtot, gridDim.x) - wg0)
+				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+#else
+	const uint64_t wg0 = prop ? (uint64_t)blockIdx.x * Rtot / gridDim.x : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+#endif
+	if (wg0 >= Rtot)
+		return false; // whole workgroup idle (small batch)
+	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
+	// equal contiguous pieces (age-weighted shares measured no better,
+	// profiles/r01/ab_v5.txt).
+#ifndef PECH_FAST_DIV
+	const uint32_t wg_rows = prop ? (uint32_t)((uint64_t)(blockIdx.x + 1u) * Rtot / gridDim.x - wg0)
+				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
+#endif
+	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
+	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
+	// Uniform batches: a wave starts on its share's head [r0, t) and then
+	// takes items of PECH_ITEM_ROWS rows from the workgroup's pool of share
+	// tails (at most PECH_POOL_ROWS of each share; an LDS counter, claim c is
+	// tail item c/16 of share c%16, located by division), so the CU's 16
+	// waves -- issued oldest-first, which made equal static shares finish up
+	// to 60 us apart -- end together, and the CU is free for the next
+	// launch's workgroup that much earlier.  (The fused copy keeps static
+	// shares: pooled items cost it 9-14 % per launch, profiles/r02/ab_item_pool.txt.)
+	// Shares below PECH_POOL_MIN_SHARE rows keep static shares too: a 512-row
+	// share (256 MiB of 64 KiB-4 MiB buffers) pooled is a 256-row head and one
+	// item, i.e. runs of 32 rows with a fold each; static, one step of 64-row
+	// runs: 48.8 instead of 51.5-53.4 us per launch (profiles/r03/ab_pool_min_share.txt).
+#ifdef PECH_NO_POOL // A/B: static shares for every batch
+	const uint32_t jmax = 0u;
+#else
+	const uint32_t jmax = !COPY && !il && uniform && wg_rows >= PECH_MAIN_WAVES * PECH_POOL_MIN_SHARE
+				      ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
+										      PECH_MAIN_WAVES) + PECH_ITEM_ROWS - 1u) /
+							     PECH_ITEM_ROWS
+					       : 0u;
+#endif
+	st.U0 = 0;
+	st.wg_rows = wg_rows;
+	st.r0 = r0;
+	st.r1 = r1;
+	st.jmax = jmax;
+	st.rem_all = jmax ? share_head(r0, r1) - r0 : r1 - r0;
+	st.wg0 = wg0;
+	st.uniform = uniform;
+	st.il = il;
+	return true;
+}
 
 // The main kernel's chunk scan and start search, with CPL chunks per lane
 // (4: batches of up to 256 chunks, 16: up to PECH_MAX_CHUNKS).  Every wave
@@ -1111,56 +1264,9 @@ __device__ __forceinline__ bool prologue_start(uint32_t *lds, const pech_core *_
 #ifdef PECH_STAMPS
 	st.t_scan = t_scan;
 #endif
-	// Every wave gets an equal share of the batch's rows (at least rpw_min).
-	// Large batches: workgroup b gets rows [b Rtot / G, (b+1) Rtot / G) --
-	// proportional, not b * ceil(Rtot / W): the rounding drifted by up to a
-	// row per wave, a whole step of 8 small buffers after a few hundred
-	// waves, so some waves walked an extra step (2 -> 3 on unaligned
-	// 4,100-byte buffers) and set the launch's end.  Small batches: shares
-	// of rpw_min rows, the last workgroups idle.
-	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_min;
-	const uint32_t rpw = prop ? 0u : rpw_min;
-#ifdef PECH_FAST_DIV // A/B: 32-bit quotients when the products fit 32 bits (batches below 4 GiB / grid rows)
-	const uint64_t wg0 = prop ? div_u64_u32((uint64_t)blockIdx.x * Rtot, gridDim.x)
-				  : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
-	const uint32_t wg_rows = prop ? (uint32_t)(div_u64_u32((uint64_t)(blockIdx.x + 1u) * Rtot, gridDim.x) - wg0)
-				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
-#else
-	const uint64_t wg0 = prop ? (uint64_t)blockIdx.x * Rtot / gridDim.x : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
-#endif
-	if (wg0 >= Rtot)
+	if (!wave_share<COPY>(Rtot, W, rpw_min, wave, uniform, il, st))
 		return false; // whole workgroup idle (small batch)
-	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
-	// equal contiguous pieces (age-weighted shares measured no better,
-	// profiles/r01/ab_v5.txt).
-#ifndef PECH_FAST_DIV
-	const uint32_t wg_rows = prop ? (uint32_t)((uint64_t)(blockIdx.x + 1u) * Rtot / gridDim.x - wg0)
-				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
-#endif
-	const uint32_t r0 = (uint32_t)(wg0 + (uint64_t)wg_rows * wave / PECH_MAIN_WAVES);
-	const uint32_t r1 = (uint32_t)(wg0 + (uint64_t)wg_rows * (wave + 1u) / PECH_MAIN_WAVES);
-	// Uniform batches: a wave starts on its share's head [r0, t) and then
-	// takes items of PECH_ITEM_ROWS rows from the workgroup's pool of share
-	// tails (at most PECH_POOL_ROWS of each share; an LDS counter, claim c is
-	// tail item c/16 of share c%16, located by division), so the CU's 16
-	// waves -- issued oldest-first, which made equal static shares finish up
-	// to 60 us apart -- end together, and the CU is free for the next
-	// launch's workgroup that much earlier.  (The fused copy keeps static
-	// shares: pooled items cost it 9-14 % per launch, profiles/r02/ab_item_pool.txt.)
-	// Shares below PECH_POOL_MIN_SHARE rows keep static shares too: a 512-row
-	// share (256 MiB of 64 KiB-4 MiB buffers) pooled is a 256-row head and one
-	// item, i.e. runs of 32 rows with a fold each; static, one step of 64-row
-	// runs: 48.8 instead of 51.5-53.4 us per launch (profiles/r03/ab_pool_min_share.txt).
-#ifdef PECH_NO_POOL // A/B: static shares for every batch
-	const uint32_t jmax = 0u;
-#else
-	const uint32_t jmax = !COPY && !il && uniform && wg_rows >= PECH_MAIN_WAVES * PECH_POOL_MIN_SHARE
-				      ? 1u + (min(PECH_POOL_ROWS, (wg_rows + PECH_MAIN_WAVES - 1u) /
-										      PECH_MAIN_WAVES) + PECH_ITEM_ROWS - 1u) /
-							     PECH_ITEM_ROWS
-					       : 0u;
-#endif
-	uint32_t rem_all = jmax ? share_head(r0, r1) - r0 : r1 - r0;
+	const uint32_t r0 = st.r0, rem_all = st.rem_all;
 	// nz table for plan_step: every wave writes all of it (the same values)
 	// and reads back only its own writes until the barrier below
 #pragma unroll
@@ -1252,30 +1358,134 @@ __device__ __forceinline__ bool prologue_start(uint32_t *lds, const pech_core *_
 #endif
 	}
 	st.U0 = U0;
-	st.wg_rows = wg_rows;
-	st.r0 = r0;
-	st.r1 = r1;
-	st.jmax = jmax;
-	st.rem_all = rem_all;
 	st.p0 = p0;
 	st.lr0 = lr0;
 	st.jj = jj;
 	st.pjj = pjj;
 	st.nzjj = nzjj;
 	st.nsjj = nsjj;
-	st.wg0 = wg0;
-	st.uniform = uniform;
-	st.il = il;
 	return true;
 }
 
-template <bool COPY, uint32_t U>
+// The flat prologue (pech_crc32c_flat): lane l holds descriptors 4l .. 4l+3
+// (dv, loaded at entry with the tables).  Every wave computes their rows,
+// scans them itself (DPP), takes its share (wave_share) and finds the
+// position holding its first row with one ballot -- no plan kernel, no
+// workspace reads.  It also writes the batch's LDS table (flat_core): all of
+// it, the same values in every wave, read back only from its own writes
+// until the workgroup's barrier.  Rtot: the launch's rows (the early table
+// fill's exact size).  Uniform (every buffer the same rows, none empty):
+// position p holds rows [p U0, (p+1) U0), as the pool needs.
+__device__ __forceinline__ bool prologue_flat(uint32_t *lds, const u32x4 (&dv)[4], uint32_t n, uint32_t lane,
+					      uint32_t wave, uint32_t W, uint32_t rpw_min, Start &st, uint32_t &Rtot)
+{
+	uint32_t rows[4], lsum = 0;
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k) {
+		const uint32_t p = 4u * lane + k, lb = dv[k].x & (PECH_ROW_BYTES - 1u), len = dv[k].z;
+		rows[k] = p < n && len ? (uint32_t)(((uint64_t)lb + len + PECH_ROW_BYTES - 1u) >> 7) : 0u;
+		lsum += rows[k];
+		if (p < n) { // T: zero bytes after the buffer in its last line
+			const uint32_t T = rows[k] ? rows[k] * PECH_ROW_BYTES - lb - len : 0u;
+			*(u32x4 *)(lds + L_FLAT / 4u + 4u * p) = u32x4{dv[k].x, dv[k].y, rows[k], p | T << 20};
+		}
+	}
+	const uint32_t incl = wave_incl_scan(lsum);
+	Rtot = lane_value(incl, 63);
+	const uint32_t U0 = lane_value(rows[0], 0);
+	bool uok = true;
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k)
+		uok = uok && (4u * lane + k >= n || rows[k] == U0);
+	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
+	if (!wave_share<false>(Rtot, W, rpw_min, wave, uniform, false, st))
+		return false; // whole workgroup idle (small batch)
+	st.U0 = U0;
+	st.p0 = st.lr0 = 0;
+	st.jj = st.pjj = st.nzjj = st.nsjj = 0;
+	if (st.rem_all) {
+		// the one position p with prefix(p) <= r0 < prefix(p) + rows(p)
+		const uint32_t r0 = st.r0;
+		uint32_t pre = incl - lsum, hk = 4u, lr = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			const bool h = rows[k] != 0u && pre <= r0 && r0 - pre < rows[k];
+			hk = h ? k : hk;
+			lr = h ? r0 - pre : lr;
+			pre += rows[k];
+		}
+		const uint32_t L = (uint32_t)__builtin_ctzll(__ballot(hk < 4u) | (1ull << 63));
+		st.p0 = 4u * L + lane_value(hk, L);
+		st.lr0 = lane_value(lr, L);
+#ifdef PECH_DEBUG_BOUNDS
+		if (lane == 0 && (st.p0 >= n || lane_value(hk, L) >= 4u))
+			printf("PECH OOB flat prologue blk %u wave %u r0 %u p0 %u n %u\n", blockIdx.x, wave, r0, st.p0, n);
+#endif
+	}
+	return true;
+}
+
+// FLAT (pech_crc32c_flat): the same walk for n <= PECH_FLAT_MAX buffers with
+// no plan kernel -- the descriptors are read at entry (descs) and kept in LDS
+// (prologue_flat), and out[] is zeroed by workgroup 0 and published through
+// *flag = tag (below).
+// Flat batches, workgroup 0's first wave, after its zeroes are published:
+// the seed terms x^(8 len) s of R(s, D) = x^(8|D|) s ^ R(0, D), and the seed
+// itself for an empty buffer, XORed into out[] (the messenger's seeds are 0:
+// nothing to do).
+__device__ __forceinline__ void flat_seeds(const u32x4 (&dv)[4], uint32_t n, uint32_t lane,
+					   const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
+{
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k) {
+		const uint32_t p = 4u * lane + k, len = dv[k].z, seed = dv[k].w;
+		if (p < n && seed != 0u)
+			atomicXor(out + p, len ? shift_bytes(consts + PECH_C_POWB, len, seed) : seed);
+	}
+}
+
+// The other waves of a flat launch see out[] zeroed once *flag holds this
+// launch's tag.  Their early load (issued just before the ring's prime and
+// consumed behind it, so it costs no wait) normally already returns it, and
+// `ready` is set then; otherwise this polls, once per wave, before its
+// first XOR into out[].  No acquire fence: every access to out[] in the
+// launch is a device-scope atomic (the zeroes too), ordered at the word
+// itself, and the XORs are issued only after the tag was read.  (An acquire
+// here was an L2 invalidate per wave: +6.5 us per C3 launch.)
+__device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &ready)
+{
+	if (ready)
+		return;
+	// (bounded: a wave never waits forever -- ~1 s, then it goes on, and the
+	// bounds-checked build reports it; workgroup 0 is dispatched before any
+	// workgroup of its XCD, so in practice the tag is there within
+	// microseconds).  Each poll is consumed before the loop can exit, so no
+	// load of this rare path is left pending at the step loop's join, where
+	// the compiler would wait for it with a vmcnt(0) -- a drain of the ring
+	// at every step end.
+	for (uint32_t spin = 0;; ++spin) {
+		const uint64_t v = uni64(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+		if (v == tag || spin >= (1u << 24)) {
+#ifdef PECH_DEBUG_BOUNDS
+			if (v != tag && (threadIdx.x & 63u) == 0)
+				printf("PECH OOB flat tag never published blk %u\n", blockIdx.x);
+#endif
+			break;
+		}
+		__builtin_amdgcn_s_sleep(2);
+	}
+	ready = true;
+}
+
+template <bool COPY, uint32_t U, bool FLAT = false>
 __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
 					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
 					  const uint32_t *__restrict__ nzs, uint32_t n,
 					  const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min,
-					  const int64_t *__restrict__ deltas)
+					  const int64_t *__restrict__ deltas, const pech_desc *__restrict__ descs = nullptr,
+					  uint64_t *flag = nullptr, uint64_t tag = 0)
 {
+	static_assert(!(FLAT && COPY), "flat batches: CRC only");
 	const uint32_t tid = threadIdx.x;
 	STAMP(t_entry);
 #ifdef PECH_KARGS_AT_ENTRY
@@ -1290,6 +1500,24 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t wave = uni(tid >> 6);
 	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 	const uint32_t nchunks = (n + PECH_CHUNK - 1u) / PECH_CHUNK;
+	if constexpr (FLAT) {
+		// Workgroup 0's first wave zeroes out[] and publishes it, first thing:
+		// *flag = tag, a release store at device scope once the zeroes are
+		// done (atomic exchanges: every access to out[] in the launch is a
+		// device-scope atomic).  The other waves XOR their runs into out[]
+		// only once they have seen the tag (flat_ready), so no plan kernel
+		// has to initialise out[].  The host gives every flat launch a fresh
+		// 64-bit tag; graph captures, whose replays would repeat it, take the
+		// planned path.
+		if (blockIdx.x == 0 && wave == 0) {
+#pragma unroll
+			for (uint32_t k = 0; k < 4; ++k)
+				if (4u * lane + k < n)
+					(void)atomicExch(out + 4u * lane + k, 0u);
+			if (lane == 0)
+				__hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+		}
+	}
 
 	// Prologue (v0.11): three dependent global rounds before the first data
 	// instead of four, and no barrier until the ring is primed.  Every wave
@@ -1328,33 +1556,42 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifndef PECH_CONSTS_LAST
 	load_consts();
 #endif
-	const uint32_t rows0 = uni(partials[0]); // chunk 0's rows (the early fill's launch-size estimate)
-	// the speculative start (below), its chunk's row offsets, then the chunk totals
-	u32x4 lr4[4];
-	const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
-	// likely start position: exact for uniform batches (a double quotient of
-	// integers is exact when it is one; a near miss only costs a reload)
-	const uint32_t pg = uni(min((uint32_t)((double)wglob * (double)n / (double)W), n - 1u));
-	const uint32_t cg = pg >> 10;                                   // and chunk
-	const uint32_t lrg = lrs[pg]; // pg's row offset in its chunk
-	// cores[pg + grp] (pg + 7 may run into lrs: workspace memory, used only if in the chunk)
-	const pech_core spec = load_spec(cores, pg + grp);
-
-	// the speculative row offsets.  Unconditional -- a load under a branch
-	// gets a vmcnt(0) at the join -- with lanes past the chunk's buffers
-	// reading lane 0's lines (no extra traffic; masked later).
-#ifndef PECH_LR4_LAZY
-	{
-		const uint32_t ll = lane * 16u < n - cg * PECH_CHUNK ? lane : 0u;
+	uint32_t rows0 = 0, pg = 0, cg = 0, lrg = 0;
+	pech_core spec = pech_core{};
+	u32x4 lr4[4], dv[4];
+	if constexpr (FLAT) {
+		// the batch's descriptors, 4 per lane (64 contiguous bytes), with the tables
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k)
-			lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + ll * 16u))[k];
-	}
+			dv[k] = ((const u32x4 *)descs)[min(4u * lane + k, n - 1u)];
+	} else {
+		rows0 = uni(partials[0]); // chunk 0's rows (the early fill's launch-size estimate)
+		// the speculative start (below), its chunk's row offsets, then the chunk totals
+		const uint32_t wglob = blockIdx.x * PECH_MAIN_WAVES + wave;
+		// likely start position: exact for uniform batches (a double quotient of
+		// integers is exact when it is one; a near miss only costs a reload)
+		pg = uni(min((uint32_t)((double)wglob * (double)n / (double)W), n - 1u));
+		cg = pg >> 10;   // and chunk
+		lrg = lrs[pg]; // pg's row offset in its chunk
+		// cores[pg + grp] (pg + 7 may run into lrs: workspace memory, used only if in the chunk)
+		spec = load_spec(cores, pg + grp);
+
+		// the speculative row offsets.  Unconditional -- a load under a branch
+		// gets a vmcnt(0) at the join -- with lanes past the chunk's buffers
+		// reading lane 0's lines (no extra traffic; masked later).
+#ifndef PECH_LR4_LAZY
+		{
+			const uint32_t ll = lane * 16u < n - cg * PECH_CHUNK ? lane : 0u;
+#pragma unroll
+			for (uint32_t k = 0; k < 4; ++k)
+				lr4[k] = ((const u32x4 *)(lrs + cg * PECH_CHUNK + ll * 16u))[k];
+		}
 #else
 #pragma unroll
-	for (uint32_t k = 0; k < 4; ++k)
-		lr4[k] = (u32x4)(0u);
+		for (uint32_t k = 0; k < 4; ++k)
+			lr4[k] = (u32x4)(0u);
 #endif
+	}
 #ifdef PECH_CONSTS_LAST // A/B: the tables' loads after the ones the scan and the start search wait for
 	load_consts();
 #endif
@@ -1406,20 +1643,37 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// from the waves still in their prologue and the tail grew
 	// (profiles/r04/ab_early_fill.txt).  The copy kernel's table depends on
 	// the scan (interleaved mode): late fill.
-	const bool early_fill = !COPY && !PECH_IL_CRC &&
-				(uint64_t)rows0 * nchunks <= (uint64_t)PECH_EARLY_FILL_ROWS * gridDim.x; // workgroup-uniform
-	if (early_fill) {
-		fill_tables(false);
-		__syncthreads();
-	}
+	// (Flat batches know the launch's rows exactly before they decide: the
+	// scan of their descriptors needs no further load.)
 	Start sv;
-	const bool live = nchunks <= 64u * 4u
-			  ? prologue_start<COPY, 4>(lds, cores, lrs, partials, nzs, n, nchunks, lane, wave, W, rpw_min, pg,
-						    cg, lrg, spec, lr4, sv)
-			  : prologue_start<COPY, 16>(lds, cores, lrs, partials, nzs, n, nchunks, lane, wave, W, rpw_min, pg,
-						     cg, lrg, spec, lr4, sv);
-	if (!live)
-		return; // whole workgroup idle (small batch)
+	bool early_fill, live;
+	if constexpr (FLAT) {
+		uint32_t Rtot;
+		live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot);
+		if (blockIdx.x == 0 && wave == 0)
+			flat_seeds(dv, n, lane, consts, out);
+		if (!live)
+			return; // whole workgroup idle (small batch)
+		early_fill = !PECH_IL_CRC && Rtot <= (uint64_t)PECH_EARLY_FILL_ROWS * gridDim.x; // workgroup-uniform
+		if (early_fill) {
+			fill_tables(false);
+			__syncthreads();
+		}
+	} else {
+		early_fill = !COPY && !PECH_IL_CRC &&
+			     (uint64_t)rows0 * nchunks <= (uint64_t)PECH_EARLY_FILL_ROWS * gridDim.x; // workgroup-uniform
+		if (early_fill) {
+			fill_tables(false);
+			__syncthreads();
+		}
+		live = nchunks <= 64u * 4u
+			       ? prologue_start<COPY, 4>(lds, cores, lrs, partials, nzs, n, nchunks, lane, wave, W, rpw_min, pg,
+							 cg, lrg, spec, lr4, sv)
+			       : prologue_start<COPY, 16>(lds, cores, lrs, partials, nzs, n, nchunks, lane, wave, W, rpw_min,
+							  pg, cg, lrg, spec, lr4, sv);
+		if (!live)
+			return; // whole workgroup idle (small batch)
+	}
 #ifdef PECH_STAMPS
 	const uint64_t t_scan = sv.t_scan;
 #endif
@@ -1439,7 +1693,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// last step per wave, with idle groups (unaligned 4,100-byte buffers: 2
 	// steps per wave became 3, +37 % per launch), and ownership by the first
 	// row flipped with +-1 row of jitter when shares and steps nearly align.
-	const bool grid = jmax == 0u;
+	const bool grid = !FLAT && jmax == 0u; // (flat batches keep descriptor order: no size classes)
 	if (grid && rem_all) {
 		const uint32_t local = p0 & 1023u;
 		if (local < nsjj) {
@@ -1463,8 +1717,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		lr0 = (uint32_t)(wg0 - (uint64_t)p0 * U0);
 		rem_all = wg_rows;
 	}
-	Step S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
-		    : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
+	Step S;
+	if constexpr (FLAT)
+		S = plan_step<false, false, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false, pech_core{}, 0u, n);
+	else
+		S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
+		       : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
 	STAMP(t_plan);
 	uint32_t tpow = COPY ? 0u : rowpow(consts, S); // x^(8 128 ra) of the step's run (finish_run)
 	// Static shares walk on from where a step ends: the CRC kernel loads the
@@ -1480,8 +1738,20 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	uint32_t nppos = COPY ? 0u : min(S.pos, nslots - 1u);
 	pech_core nspec = COPY ? pech_core{} : load_spec(cores, nppos + grp);
 #endif
-	if (S.T)
+	// Flat: workgroup 0 zeroed out[] itself (its first wave, before the
+	// barrier below); every other wave reads the flag now, just before its
+	// prime, and looks at it behind the prime's first row (below)
+	// (one straight-line block, so the wait for the flag counts the prime's
+	// loads after it: vmcnt(7), not a drain)
+	uint64_t seen = 0;
+	bool ready = !FLAT || blockIdx.x == 0;
+	if (S.T) {
+		if (FLAT)
+			seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		RING_PRIME_RS(S, ring, rsb);
+		if (FLAT)
+			ready = ready || uni64(seen) == tag;
+	}
 
 	// otherwise the tables are written while the prime is in flight
 	if (!early_fill)
@@ -1571,7 +1841,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			for (uint32_t i = 0; i < U; ++i) {
 				ring[(i + U - 1) % U] =
 					LD_PIECE(S, row_addr(S.ad, min(r + i + U - 1, last), STEP_ZOFF(S), rsb), 3);
-				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+				horner_row_pred(lds, lreg, zl_mask<FLAT>(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 				st_piece<COPY>(S, r + i, ring[i],
 					       r + i < S.nu && (r + i != 0 || !STEP_HEAD(S)) && zl_keep(S, r + i), rsb);
 			}
@@ -1611,10 +1881,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			}
 		}
 #ifndef PECH_NO_NEXT_SPEC
-		const Step N = il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
+		const Step N = FLAT ? plan_step<false, false, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, false,
+								    pech_core{}, 0u, n)
+			   : il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 			   : COPY ? plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid)
 				  : plan_step<COPY, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid, nspec, nppos);
-		if (!COPY) { // the descriptors where the step after N starts
+		if (!COPY && !FLAT) { // the descriptors where the step after N starts (flat: they are in LDS)
 			nppos = min(N.pos, nslots - 1u);
 			if (jmax > 1u && N.rem == 0) {
 				// N ends a pooled item: the next item is the pending claim's
@@ -1629,7 +1901,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			nspec = load_spec(cores, nppos + grp);
 		}
 #else // A/B: N's descriptors loaded when N is planned
-		const Step N = il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
+		const Step N = FLAT ? plan_step<false, false, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, false,
+								    pech_core{}, 0u, n)
+			   : il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 				  : plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
 #endif
 		const uint32_t tpow_n = COPY ? 0u : rowpow(consts, N); // (used when N ends)
@@ -1650,7 +1924,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			for (uint32_t i = 1; i < U; ++i)
 				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L), rsb), 5);
 		} else {
-			horner_row_pred(lds, lreg, zl_mask(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
+			horner_row_pred(lds, lreg, zl_mask<FLAT>(S, r, ring[0]), r < S.nu, s0, s1, s2, s3);
 			st_piece<COPY>(S, r, ring[0], r < S.nu && (r != 0 || !STEP_HEAD(S)) && zl_keep(S, r), rsb);
 			// Branch-free on purpose: with no next step the prefetch re-reads
 			// this step's last row (valid memory, never used).  An if/else here
@@ -1662,16 +1936,16 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 			for (uint32_t i = 1; i < U; ++i) {
 				ring[i - 1] = LD_PIECE(L, row_addr(L.ad, min(lrow0 + i - 1, lmax), STEP_ZOFF(L), rsb), 5);
-				horner_row_pred(lds, lreg, zl_mask(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
+				horner_row_pred(lds, lreg, zl_mask<FLAT>(S, r + i, ring[i]), r + i < S.nu, s0, s1, s2, s3);
 				st_piece<COPY>(S, r + i, ring[i], r + i < S.nu && zl_keep(S, r + i), rsb);
 			}
 		}
 #ifdef PECH_DEBUG_BOUNDS
 		{ // debug build: an active group's output slot must lie in this launch's slots
-			const bool bad = S.nu != 0 && STEP_ORIG(S) >= nchunks * PECH_CHUNK;
+			const bool bad = S.nu != 0 && step_orig<FLAT>(S) >= (FLAT ? n : nchunks * PECH_CHUNK);
 			if (bad && g8 == 0)
-				printf("PECH OOB out blk %u wave %u orig %u nu %u T %u pos %u\n", blockIdx.x, wave, STEP_ORIG(S), S.nu,
-				       S.T, S.pos);
+				printf("PECH OOB out blk %u wave %u orig %u nu %u T %u pos %u\n", blockIdx.x, wave, step_orig<FLAT>(S),
+				       S.nu, S.T, S.pos);
 			if (bad)
 				S.nu = 0;
 		}
@@ -1679,7 +1953,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifdef PECH_STAMP_FIN // stamps build: the last step's fold + shift (75 % stamp -> its start)
 		tq[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-		finish_run<!COPY>(lds, g8, s0, s1, s2, s3, STEP_M(S), STEP_RA(S), tpow, S.nu != 0, out, STEP_ORIG(S));
+		if (FLAT)
+			flat_ready(flag, tag, ready);
+		finish_run<!COPY>(lds, g8, s0, s1, s2, s3, step_m<FLAT>(S), STEP_RA(S), tpow, S.nu != 0, out, step_orig<FLAT>(S));
 		tpow = tpow_n;
 #ifdef PECH_STAMP_FIN
 		tq[1] = __builtin_amdgcn_s_memrealtime();
@@ -1702,10 +1978,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		__threadfence_block();
 		static_assert(PECH_DEFER_SLOTS == 64u, "one slot per lane of the flushing wave");
 		if (done == PECH_MAIN_WAVES - 1u) {
+			if (FLAT)
+				flat_ready(flag, tag, ready);
 			const uint32_t k = lds[L_DEFER / 4u + lane];
 			bool flush = k != PECH_DEFER_EMPTY;
 #ifdef PECH_DEBUG_BOUNDS
-			if (flush && k >= nchunks * PECH_CHUNK) {
+			if (flush && k >= (FLAT ? n : nchunks * PECH_CHUNK)) {
 				printf("PECH OOB flush blk %u slot %u key %u\n", blockIdx.x, lane, k);
 				flush = false;
 			}
@@ -1754,6 +2032,22 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 {
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	main_body<true, PECH_U_COPY>(lds, cores, lrs, partials, nzs, n, consts, out, rpw_min, deltas);
+}
+
+// One-launch device batch of up to PECH_FLAT_MAX buffers (any sizes): the
+// main kernel's walk with no plan kernel (main_body<FLAT>).  A batch of few
+// buffers -- C3's 256 x 4 MiB, an async slot of large payloads, a single
+// large message -- then costs one launch on the stream instead of two, and
+// its prologue reads the descriptors themselves instead of the plan's
+// workspace.  `flag` (8 bytes of the caller's workspace) and the per-launch
+// `tag` publish workgroup 0's zeroed out[] to the other workgroups.
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_flat(
+	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	uint32_t rpw_min, uint64_t *__restrict__ flag, uint64_t tag)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
+	main_body<false, PECH_U, true>(lds, nullptr, nullptr, nullptr, nullptr, n, consts, out, rpw_min, nullptr, descs, flag,
+				       tag);
 }
 
 // ---- direct kernel: small-buffer batches without a plan kernel -------------
@@ -2179,6 +2473,19 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 	return hipGetLastError();
 }
 
+// flat kernel (one launch, 1 <= n <= PECH_FLAT_MAX); ev_start/ev_stop as
+// pech_launch_main; flag: 8-byte aligned device word, tag: fresh per launch
+extern "C" hipError_t pech_launch_flat(const pech_desc *descs, uint32_t n, const uint32_t *consts, uint32_t *out,
+				       uint32_t ncu, uint32_t rpw_min, uint64_t *flag, uint64_t tag, hipStream_t stream,
+				       hipEvent_t ev_start, hipEvent_t ev_stop)
+{
+	if (n == 0 || n > PECH_FLAT_MAX || ((uintptr_t)flag & 7u))
+		return hipErrorInvalidValue;
+	hipExtLaunchKernelGGL(pech_crc32c_flat, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u, descs,
+			      n, consts, out, rpw_min, flag, tag);
+	return hipGetLastError();
+}
+
 // direct kernel (no plan, no workspace); ev_start/ev_stop as pech_launch_main;
 // dsts != NULL: the fused-copy variant
 extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, const uint32_t *consts, uint32_t *out,
@@ -2198,6 +2505,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.28 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.29 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

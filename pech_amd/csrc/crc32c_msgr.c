@@ -470,6 +470,11 @@ void crc32c_msgr_conn_reset(struct crc32c_msgr_conn *c)
 	c->npending = 0;
 }
 
+struct crc32c_async *crc32c_msgr_conn_async(const struct crc32c_msgr_conn *c)
+{
+	return c ? c->a : NULL;
+}
+
 void crc32c_msgr_conn_destroy(struct crc32c_msgr_conn *c)
 {
 	if (!c)

@@ -70,6 +70,9 @@
 #define PECH_NZ_UNIFORM 0x80000000u /* nzs[] flag: every buffer of the chunk has a core of the same rows */
 #define PECH_NZ_MASK 0x7FFu         /* nzs[] bits 0-10: non-empty cores of the chunk */
 #define PECH_NS_SHIFT 11u           /* nzs[] bits 11-21: of them, cores below PECH_SPLIT_ROWS (sorted first) */
+#ifndef PECH_FLAT_MAX
+#define PECH_FLAT_MAX 256u        /* device batches of up to this many buffers: one launch, no plan kernel */
+#endif
 #define PECH_SMALL_MAX 65536u     /* drop-in crc32c(): one-launch path up to this */
 #define PECH_DROPIN_CPU_MAX_DEFAULT (4u << 20) /* drop-in crc32c(): host routine up to this */
 /* payload of one launch: rows (128 B) are counted in 32 bits, so < 512 GiB */
@@ -150,7 +153,10 @@ LAYOUT_FN uint32_t pech_size_class(uint32_t rows)
  *   partials u32[PECH_MAX_CHUNKS]    rows per chunk
  *   nzs      u32[PECH_MAX_CHUNKS]    non-empty cores per chunk | small ones << 11 | PECH_NZ_UNIFORM
  *   deltas   i64[slots]              fused copy: destination - source per buffer
- * slots = nch * PECH_CHUNK, nch = ceil(m / PECH_CHUNK). */
+ * slots = nch * PECH_CHUNK, nch = ceil(m / PECH_CHUNK).
+ * A flat launch (m <= PECH_FLAT_MAX, no plan kernel) uses only the first
+ * 8 bytes: the u64 word through which its workgroup 0 publishes the zeroed
+ * out[] (crc32c_kernels.hip, pech_crc32c_flat). */
 struct pech_ws {
 	struct pech_core *cores;
 	uint32_t *lrs, *partials, *nzs;

@@ -44,7 +44,11 @@
  *     revoked ones included) is freed by teardown, after ceph_msgr_exit()
  *     has drained the async context;
  *   - with --expect-gpu: the adapter's counters show GPU submissions on
- *     both sides (payloads above its 8 KiB host cutoff), and none in nocrc.
+ *     both sides (payloads above its 8 KiB host cutoff), and none in nocrc;
+ *   - with --expect-contexts N: the patch created N async contexts (one per
+ *     entry of PECH_DEVICES, e.g. "0,0": two on one GPU) and, unless nocrc,
+ *     every one of them took submissions -- the connections are spread
+ *     over them (recorded by wrapping crc32c_async_create_on).
  *
  * Scenarios (argv[1]): basic | corrupt-req | corrupt-reply | revoke | nocrc
  */
@@ -108,7 +112,9 @@ struct lb_srv_con {
 
 static struct {
 	const char *scenario;
-	int expect_gpu, nocrc;
+	int expect_gpu, nocrc, expect_ctx;
+	struct crc32c_async *ctx[16]; /* the patch's async contexts, in creation order */
+	int nctx;
 	struct ceph_options *opt;
 	struct ceph_messenger srv, cli;
 	struct ceph_connection ccon;
@@ -437,6 +443,18 @@ int __wrap_crc32c_msgr_tx_footer(struct crc32c_msgr_conn *c, void *msg, uint32_t
 	return ret;
 }
 
+/* every async context the patch creates (crc_ctx_init: one per device) */
+struct crc32c_async *__real_crc32c_async_create_on(int device, unsigned int flags);
+
+struct crc32c_async *__wrap_crc32c_async_create_on(int device, unsigned int flags)
+{
+	struct crc32c_async *a = __real_crc32c_async_create_on(device, flags);
+
+	if (a && S.nctx < (int)ARRAY_SIZE(S.ctx))
+		S.ctx[S.nctx++] = a;
+	return a;
+}
+
 static void revoke_workfn(struct work_struct *w)
 {
 	struct lb_req *r;
@@ -484,6 +502,7 @@ static int lb_task(void *arg)
 	struct sockaddr_storage ss;
 	struct sockaddr_in *sin;
 	struct crc32c_msgr_stats st;
+	struct crc32c_async_stats cst[16];
 	u16 srv_port, relay_port;
 	int i, ret, corrupt_idx = -1, revoke_idx = -1, revoked_mid = 0;
 	struct ceph_msg *last_out = NULL;
@@ -592,6 +611,8 @@ static int lb_task(void *arg)
 	for (i = 0; i < S.nreq; i++)
 		ceph_msg_put(S.req[i].m);
 	crc32c_msgr_get_stats(&st);
+	for (i = 0; i < S.nctx; i++)
+		crc32c_async_get_stats(S.ctx[i], &cst[i]);
 	/* the patch's _ceph_msgr_exit: the async context is destroyed first
 	 * (drained: orphaned CRCs land and release their messages) */
 	ceph_msgr_exit();
@@ -617,6 +638,16 @@ static int lb_task(void *arg)
 		if (S.expect_gpu)
 			ok = ok && (S.nocrc ? gpu_sub == 0 : st.rx_submitted > 0 && st.tx_submitted > 0) &&
 			     (corrupt_idx < 0 || st.rx_bad >= 1);
+		if (S.expect_ctx) {
+			ok = ok && S.nctx == S.expect_ctx;
+			for (i = 0; i < S.nctx; i++)
+				ok = ok && (S.nocrc ? cst[i].submitted == 0 : cst[i].submitted > 0);
+		}
+		printf("{\"contexts\": [");
+		for (i = 0; i < S.nctx; i++)
+			printf("%s{\"device\": %d, \"submitted\": %llu, \"launches\": %llu}", i ? ", " : "", cst[i].device,
+			       (unsigned long long)cst[i].submitted, (unsigned long long)cst[i].launches);
+		printf("]}\n");
 		printf("{\"scenario\": \"%s\", \"ok\": %s, \"requests\": %d, \"unanswered\": %d, \"revoked_mid_send\": %d, "
 		       "\"revoked_footer_held\": %d, "
 		       "\"srv_dispatched\": %d, \"srv_dups\": %d, \"cli_dispatched\": %d, \"cli_dups\": %d, "
@@ -662,7 +693,8 @@ int main(int argc, char **argv)
 	int i;
 
 	if (argc < 2) {
-		fprintf(stderr, "usage: %s basic|corrupt-req|corrupt-reply|revoke|nocrc [--expect-gpu]\n", argv[0]);
+		fprintf(stderr, "usage: %s basic|corrupt-req|corrupt-reply|revoke|nocrc [--expect-gpu] [--expect-contexts N]\n",
+			argv[0]);
 		return 2;
 	}
 	memset(&S, 0, sizeof(S));
@@ -671,6 +703,8 @@ int main(int argc, char **argv)
 	for (i = 2; i < argc; i++)
 		if (!strcmp(argv[i], "--expect-gpu"))
 			S.expect_gpu = 1;
+		else if (!strcmp(argv[i], "--expect-contexts") && i + 1 < argc)
+			S.expect_ctx = atoi(argv[++i]);
 	setvbuf(stdout, NULL, _IONBF, 0);
 	signal(SIGABRT, on_abort);
 	signal(SIGSEGV, on_abort);

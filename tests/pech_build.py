@@ -121,8 +121,9 @@ def build_loopback(out):
         os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
         tmp = out + ".tmp"
         # the test wraps the messenger's held-footer call (revoke scenario)
+        # and its context creation (the contexts' counters)
         r = subprocess.run(["gcc", "-o", tmp, lb, px, orc, *objs, *LINK_LIBS, "-Wl,-rpath,$ORIGIN/../pech_amd",
-                            "-Wl,--wrap=crc32c_msgr_tx_footer"],
+                            "-Wl,--wrap=crc32c_msgr_tx_footer", "-Wl,--wrap=crc32c_async_create_on"],
                            capture_output=True, text=True, timeout=300)
         if r.returncode:
             raise RuntimeError(r.stderr[-3000:])

@@ -115,6 +115,64 @@ def test_async_payload_larger_than_slots():
 
 
 @pytest.mark.gpu
+def test_async_dma_wait_launches_the_next_slot():
+    # CRC32C_ASYNC_DMA keeps one slot's copies in flight; a submit that waits
+    # for a free slot harvests the oldest AND launches the next queued one
+    # (it stayed queued until complete() or the next blocking
+    # submit, so copy engine and GPU idled while the caller filled slots)
+    import pech_amd as P
+
+    rng = np.random.default_rng(8)
+    ac = P.AsyncCrc(dma=True)
+    pages = [P.Pages(11) for _ in range(17)]  # 8 MiB each: four fill a 32 MiB slot
+    got, want = {}, {}
+    for i, pg in enumerate(pages):
+        pg.view[:] = rng.integers(0, 256, pg.nbytes, dtype=np.uint8)
+        want[i] = O.crc(i, pg.view)
+        ac.submit(pg.ptr, pg.nbytes, i, lambda crc, err, i=i: got.__setitem__(i, (crc, err)))
+        st = ac.stats()
+        if i == 15:  # four slots filled: the first launched, three queued behind it
+            assert st["launches"] == 1 and st["inflight"] == 1 and st["queued"] == 3, st
+    # the 17th submit waited for the first slot: the second is launched now
+    assert st["launches"] == 2 and st["inflight"] == 1 and st["queued"] == 2, st
+    assert st["submitted"] == 17
+    ac.drain()
+    assert got == {i: (want[i], 0) for i in range(17)}
+    ac.close()
+    for pg in pages:
+        pg.free()
+
+
+@pytest.mark.gpu
+def test_async_context_per_device(monkeypatch):
+    # one context per GPU of the PECH_DEVICES list (two on one GPU here), each
+    # with its own counters; payloads spread over them complete bit-exact
+    import pech_amd as P
+
+    monkeypatch.setenv("PECH_DEVICES", "0,0")
+    devs = P.async_devices()
+    assert devs == [0, 0]
+    ctxs = [P.AsyncCrc(device=d) for d in devs]
+    rng = np.random.default_rng(9)
+    got, want, keep = {}, {}, []
+    for i in range(40):
+        b = rng.integers(0, 256, int(rng.integers(1, 3 << 20)), dtype=np.uint8)
+        keep.append(b)
+        want[i] = O.crc(0, b)
+        ctxs[i % 2].submit(b.ctypes.data, b.size, 0, lambda crc, err, i=i: got.__setitem__(i, (crc, err)), keep=b)
+    for ac in ctxs:
+        ac.drain()
+    assert got == {i: (want[i], 0) for i in range(40)}
+    for ac in ctxs:
+        st = ac.stats()
+        assert st["device"] == 0 and st["submitted"] == 20 and st["launches"] >= 1, st
+        ac.close()
+    monkeypatch.setenv("PECH_DEVICES", "0,99")
+    with pytest.raises(P.Crc32cError):
+        P.async_devices()
+
+
+@pytest.mark.gpu
 def test_pages_allocator():
     import pech_amd as P
     from pech_amd import _lib

@@ -71,7 +71,7 @@ def test_pech_osd_links_and_binds_to_library():
 
 
 # the library entry points the patched messenger calls
-ADAPTER_SYMS = {"crc32c", "crc32c_async_create", "crc32c_async_fd", "crc32c_async_flush", "crc32c_async_complete",
+ADAPTER_SYMS = {"crc32c", "crc32c_async_devices", "crc32c_async_create_on", "crc32c_msgr_conn_async", "crc32c_async_fd", "crc32c_async_flush", "crc32c_async_complete",
                 "crc32c_async_pending", "crc32c_async_destroy", "crc32c_last_error", "crc32c_msgr_conn_create",
                 "crc32c_msgr_conn_destroy", "crc32c_msgr_conn_reset", "crc32c_msgr_rx_queue", "crc32c_msgr_rx_next",
                 "crc32c_msgr_rx_pending", "crc32c_msgr_tx_submit", "crc32c_msgr_tx_has", "crc32c_msgr_tx_footer",

@@ -1,8 +1,8 @@
 """The bounds-checked kernel build (build/lib_dbg.so, -DPECH_DEBUG_BOUNDS,
 built by `make`) on C4- and C2-shaped batches with unaligned starts and
-ragged ends: every ring load (plan + main kernels, and the direct kernel of the
-small-buffer API) is checked against its buffer's rows on the
-GPU (a violation prints "PECH OOB" and is redirected instead of faulting),
+ragged ends: every ring load (plan + main kernels, the direct kernel of the
+small-buffer API, and the flat kernel of batches of up to 256 buffers) is
+checked against its buffer's rows on the GPU (a violation prints "PECH OOB" and is redirected instead of faulting),
 and every result must still equal the oracle.  Runs in a subprocess so the
 release library stays the one this test process loads."""
 import os
@@ -29,6 +29,11 @@ shape = sys.argv[2]
 if shape == "c4":
     lens = np.array([4096] * 2048 + [65536] * 128 + [1 << 20] * 8 + [4 << 20] * 2, dtype=np.int64)
     lens = lens + rng.integers(-15, 16, lens.size)       # ragged ends
+elif shape == "flat":  # <= 256 buffers: the one-launch flat kernel (full-line rows, kb masks)
+    lens = rng.integers(0, 3 << 20, 200)
+    small = rng.random(200) < 0.3
+    lens[small] = rng.integers(0, 300, int(small.sum()))
+    lens[rng.random(200) < 0.1] = 0
 else:
     lens = np.array([4096] * 8192, dtype=np.int64) + rng.integers(-33, 34, 8192)
 rng.shuffle(lens)
@@ -51,7 +56,8 @@ print("ok", lens.size, int(lens.sum()))
 
 
 @pytest.mark.parametrize("seed,shape,api", [(1, "c4", "planned"), (2, "c2", "planned"), (3, "c4", "planned"),
-                                            (4, "c2", "small"), (5, "c4", "small")])
+                                            (4, "c2", "small"), (5, "c4", "small"), (6, "flat", "planned"),
+                                            (7, "flat", "planned")])
 def test_bounds_checked_build(seed, shape, api):
     lib = os.path.join(REPO, "build", "lib_dbg.so")
     assert os.path.exists(lib), "build/lib_dbg.so is built by `make`"

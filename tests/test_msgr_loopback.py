@@ -32,7 +32,9 @@ def run(scenario, *args, env=None, timeout=150):
                        env=dict(os.environ, **(env or {})))
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert lines, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
-    res = json.loads(lines[-1])
+    res = {}
+    for l in lines:  # the contexts' counters, then the scenario's line
+        res.update(json.loads(l))
     assert r.returncode == 0 and res["ok"], json.dumps(res) + "\n" + r.stderr[-3000:]
     return res
 
@@ -59,6 +61,21 @@ def test_loopback_inline_crc(scenario):
     common(res)
     if not os.path.exists("/dev/kfd"):
         assert res["adapter"]["rx_submitted"] == res["adapter"]["tx_submitted"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scenario", SCENARIOS)
+def test_loopback_gpu_two_contexts(scenario):
+    """One async context per entry of PECH_DEVICES (the patch
+    spreads its connections over every GPU): "0,0" puts two on this box's
+    GPU, and the client's and the server's connections land on different
+    ones -- each context takes submissions, each connection's CRCs stay in
+    order in its own."""
+    res = run(scenario, "--expect-gpu", "--expect-contexts", "2", env={"PECH_DEVICES": "0,0"})
+    common(res)
+    assert len(res["contexts"]) == 2
+    for c in res["contexts"]:
+        assert c["device"] == 0 and (c["submitted"] == 0 if scenario == "nocrc" else c["submitted"] > 0), c
 
 
 @pytest.mark.gpu
