@@ -271,6 +271,18 @@ static bool capturing(hipStream_t s)
 // another run does not match either.  A graph replays its captured tag, so
 // captured batches take plan + main.
 static std::atomic<unsigned int> g_flat_max{PECH_FLAT_MAX};
+
+// rows per wave below which a launch spreads its shares wave-major
+// (crc32c_kernels.hip wave_share); PECH_RPW_MIN overrides it (A/B measurements)
+static uint32_t rpw_min()
+{
+	static const uint32_t v = [] {
+		const char *e = getenv("PECH_RPW_MIN");
+		const unsigned long r = e ? strtoul(e, nullptr, 0) : 0ul;
+		return r >= 8u && r <= 4096u ? (uint32_t)r : PECH_RPW_MIN;
+	}();
+	return v;
+}
 static std::atomic<uint64_t> g_flat_tag{0};
 static std::once_flag g_flat_tag_init;
 
@@ -323,10 +335,10 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			}
 		}
 		if (flat)
-			HIP_TRY(pech_launch_flat(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN,
+			HIP_TRY(pech_launch_flat(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, rpw_min(),
 						 (uint64_t *)ws, flat_tag(), stream, tl.a, tl.b));
 		else
-			HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, PECH_RPW_MIN,
+			HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, rpw_min(),
 						 d_dsts != nullptr, stream, tl.a, tl.b));
 		if (g_timing)
 			c->pending.push_back(tl);

@@ -1143,9 +1143,16 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 	// row per wave, a whole step of 8 small buffers after a few hundred
 	// waves, so some waves walked an extra step (2 -> 3 on unaligned
 	// 4,100-byte buffers) and set the launch's end.  Small batches: shares
-	// of rpw_min rows, the last workgroups idle.
-	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_min;
-	const uint32_t rpw = prop ? 0u : rpw_min;
+	// of rpw rows, the last ones idle.  rpw grows with the launch from
+	// rpw_min to 4 rpw_min, aiming at four live waves per CU (one per SIMD):
+	// below ~128 MiB a launch is latency-bound, and fewer, longer waves
+	// spend less of it in per-wave work (32 MiB: 15.2 -> 13.4 us,
+	// profiles/r05/ab_wave_major.txt); from W 4 rpw_min rows on, every wave
+	// of every CU streams its proportional share.
+	const uint32_t G4 = 4u * gridDim.x;
+	const uint32_t rpw_a = min(max((uint32_t)(((uint64_t)Rtot + G4 - 1u) / G4), rpw_min), 4u * rpw_min);
+	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_a;
+	const uint32_t rpw = prop ? 0u : rpw_a;
 #ifdef PECH_FAST_DIV // A/B: 32-bit quotients when the products fit 32 bits (batches below 4 GiB / grid rows)
 	const uint64_t wg0 = prop ? div_u64_u32((uint64_t)blockIdx.x * Rtot, gridDim.x)
 				  : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
@@ -1153,6 +1160,30 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 				      : (uint32_t)min((uint64_t)PECH_MAIN_WAVES * rpw, (uint64_t)Rtot - wg0);
 #else
 	const uint64_t wg0 = prop ? (uint64_t)blockIdx.x * Rtot / gridDim.x : (uint64_t)blockIdx.x * PECH_MAIN_WAVES * rpw;
+#endif
+#ifndef PECH_WG_MAJOR_SMALL
+	// Small batches, wave-major: share k = wave * G + blockIdx, so the live
+	// shares spread one or two waves per CU over every CU instead of filling
+	// the first CUs' 16 waves -- four waves to a SIMD took turns at the same
+	// VALU work (prologue, fold, shift), and a 4 MiB launch's youngest waves
+	// ended 3.5 us after its oldest (profiles/r05/stamps_flat_v29a.txt).  (Not
+	// with interleaved rows: they walk the workgroup's range together.)
+	if (!prop && !il) {
+		const uint64_t k = (uint64_t)wave * gridDim.x + blockIdx.x;
+		if ((uint64_t)blockIdx.x * rpw >= Rtot)
+			return false; // whole workgroup idle: its wave 0 has the lowest share
+		const uint64_t a = k * rpw;
+		st.r0 = (uint32_t)min(a, (uint64_t)Rtot);
+		st.r1 = (uint32_t)min(a + rpw, (uint64_t)Rtot);
+		st.wg0 = 0;
+		st.wg_rows = 0;
+		st.jmax = 0;
+		st.rem_all = st.r1 - st.r0;
+		st.U0 = 0;
+		st.uniform = uniform;
+		st.il = il;
+		return true;
+	}
 #endif
 	if (wg0 >= Rtot)
 		return false; // whole workgroup idle (small batch)
@@ -1392,6 +1423,10 @@ __device__ __forceinline__ bool prologue_flat(uint32_t *lds, const u32x4 (&dv)[4
 	}
 	const uint32_t incl = wave_incl_scan(lsum);
 	Rtot = lane_value(incl, 63);
+	STAMP(t_scan);
+#ifdef PECH_STAMPS
+	st.t_scan = t_scan;
+#endif
 	const uint32_t U0 = lane_value(rows[0], 0);
 	bool uok = true;
 #pragma unroll
@@ -1740,17 +1775,29 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #endif
 	// Flat: workgroup 0 zeroed out[] itself (its first wave, before the
 	// barrier below); every other wave reads the flag now, just before its
-	// prime, and looks at it behind the prime's first row (below)
-	// (one straight-line block, so the wait for the flag counts the prime's
-	// loads after it: vmcnt(7), not a drain)
+	// prime, and looks at it behind the tables' fill and barrier (below)
 	uint64_t seen = 0;
 	bool ready = !FLAT || blockIdx.x == 0;
-	if (S.T) {
-		if (FLAT)
-			seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if constexpr (FLAT) {
+		// Unconditional, as one block: the flag's wait below then counts the
+		// prime's loads after it (vmcnt(7)) and no ring copy joins a path
+		// without them -- with a conditional prime the compiler copied the
+		// first row's registers right after issuing it, i.e. waited for it
+		// before the tables' fill and barrier.  A wave with no step primes
+		// from the constants table (valid memory, never used).
+		if (!S.T) {
+			S.ad = (uint64_t)consts + 16u * g8;
+			S.nl = 1;
+			S.oz = 0;
+#ifdef PECH_DEBUG_BOUNDS
+			S.blo = S.ad;
+			S.bhi = S.ad + 16u;
+#endif
+		}
+		seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		RING_PRIME_RS(S, ring, rsb);
-		if (FLAT)
-			ready = ready || uni64(seen) == tag;
+	} else if (S.T) {
+		RING_PRIME_RS(S, ring, rsb);
 	}
 
 	// otherwise the tables are written while the prime is in flight
@@ -1759,6 +1806,10 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	STAMP(t_fill);
 	if (!early_fill)
 		__syncthreads(); // tables published; every wave's prime is already in flight
+	// (looked at only now, the flag's round trip hides behind the fill and
+	// the barrier)
+	if (FLAT && S.T)
+		ready = ready || uni64(seen) == tag;
 	STAMP(t_start);
 	// the wave's first pool claim, one item ahead (resolved when its first
 	// item is done)

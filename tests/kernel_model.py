@@ -214,26 +214,39 @@ def slot_cw(k, weights):
     return sum(weights[g] * min(4, max(0, k - 4 * g)) for g in range(4))
 
 
-def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None):
-    """Kernel prologue: [r0, r1) of every wave -- an equal share (at least
-    rpw_min rows) per wave, split inside a workgroup by age-rank weight."""
+def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None, il=False, by_wg=False):
+    """Kernel wave_share: [r0, r1) of every wave, workgroup by workgroup.
+    Large launches (Rtot >= W * rpw): proportional workgroup ranges, equal
+    contiguous pieces inside (by age-rank weight in the model's A/B
+    variants).  Small ones: shares of rpw rows -- rpw from rpw_min up to 4
+    rpw_min, aiming at four live waves per CU -- dealt wave-major (share k =
+    wave * ncu + workgroup), except in the fused copy's interleaved mode,
+    which walks each workgroup's contiguous range.  by_wg: a list per live
+    workgroup, and whether the launch is proportional."""
     rpw_min = rpw_min or C["PECH_RPW_MIN"]
     weights = weights or C["PECH_SLOT_W"]
     waves = waves or WAVES_PER_WG
     W = ncu * waves
-    prop = Rtot >= W * rpw_min  # kernel: proportional workgroup ranges, else rpw_min shares
-    rpw = rpw_min
+    G4 = 4 * ncu
+    rpw = min(max((Rtot + G4 - 1) // G4, rpw_min), 4 * rpw_min)
+    prop = Rtot >= W * rpw
     tot = slot_cw(waves, weights)
     out = []
     for b in range(ncu):
+        if not prop and not il:
+            if b * rpw >= Rtot:
+                continue
+            out.append([(min((w * ncu + b) * rpw, Rtot), min((w * ncu + b) * rpw + rpw, Rtot)) for w in range(waves)])
+            continue
         wg0 = b * Rtot // ncu if prop else b * waves * rpw
         if wg0 >= Rtot:
             continue
         wg_rows = (b + 1) * Rtot // ncu - wg0 if prop else min(waves * rpw, Rtot - wg0)
-        for w in range(waves):
-            out.append((wg0 + wg_rows * slot_cw(w, weights) // tot,
-                        wg0 + wg_rows * slot_cw(w + 1, weights) // tot))
-    return out
+        out.append([(wg0 + wg_rows * slot_cw(w, weights) // tot, wg0 + wg_rows * slot_cw(w + 1, weights) // tot)
+                     for w in range(waves)])
+    if by_wg:
+        return out, prop
+    return [r for wg in out for r in wg]
 
 
 IL = C["PECH_IL_GROUPS"]
@@ -302,20 +315,20 @@ def main(cores, lrs, partials, nzs, ncu, rpw_min=None, U=None, weights=None, cop
     nz = [z & NZ_MASK for z in nzs]
     U0 = partials[0] // nz[0] if nz and nz[0] else 0
     uniform = bool(U0) and all((z & NZ_UNIFORM) and n * U0 == p for z, n, p in zip(nzs, nz, partials))
-    ranges = wave_ranges(Rtot, ncu, rpw_min, weights)
-    if copy and uniform and U0 >= IL_MIN:  # fused copy: interleaved rows over each workgroup's range
-        for w0 in range(0, len(ranges), WAVES_PER_WG):
-            shares = ranges[w0:w0 + WAVES_PER_WG]
+    il = copy and uniform and U0 >= IL_MIN
+    wgs, prop = wave_ranges(Rtot, ncu, rpw_min, weights, il=il, by_wg=True)
+    if il:  # fused copy: interleaved rows over each workgroup's range
+        for shares in wgs:
             wg0, wg_rows = shares[0][0], shares[-1][1] - shares[0][0]
             if wg_rows:
                 walk_il(cores, wg0 // U0, wg0 % U0, wg_rows, U, events)
         return events
-    for w0 in range(0, len(ranges), WAVES_PER_WG):
-        shares = ranges[w0:w0 + WAVES_PER_WG]
+    for shares in wgs:
         wg_rows = shares[-1][1] - shares[0][0]
-        # (shares below POOL_MIN rows keep static shares)
+        # (shares below POOL_MIN rows keep static shares; wave-major small
+        # launches never pool)
         jmax = (1 + (min(POOL, (wg_rows + WAVES_PER_WG - 1) // WAVES_PER_WG) + ITEM - 1) // ITEM
-                if uniform and wg_rows >= WAVES_PER_WG * POOL_MIN else 0)
+                if prop and uniform and wg_rows >= WAVES_PER_WG * POOL_MIN else 0)
         for r0, r1 in shares:
             if r1 > r0:
                 pos, lr = find_start(lrs, pref, nzs, r0)

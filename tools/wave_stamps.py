@@ -8,6 +8,8 @@ sys.path.insert(0, REPO)
 import pech_amd as P
 from pech_amd import _lib
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+if os.environ.get("PECH_FLAT_MAX"):  # 0: the planned path (plan + main) for batches of <= 256 buffers
+    P.set_flat_max(int(os.environ["PECH_FLAT_MAX"]))
 dev = torch.device("cuda:0")
 if cfg == "c3":
     sizes = np.full(256, 4 << 20, dtype=np.int64)
