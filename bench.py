@@ -229,7 +229,8 @@ def main():
         batch i on stream i % nstreams (own workspace) of every shard.  A
         batch's output buffer is only ever written from one stream, so steps
         never race.  Returns (elapsed seconds, max over ranks; per-launch
-        main-kernel us)."""
+        main-kernel us; this rank's own elapsed seconds; seconds its host
+        thread spent issuing the K steps)."""
         if rotate % nstreams:
             raise SystemExit(f"{nstreams} streams must divide the {rotate} rotating batches")
 
@@ -248,10 +249,12 @@ def main():
         t0 = time.perf_counter()
         for i in range(steps):
             step(i)
+        issue = time.perf_counter() - t0  # (the host thread's issue time: no wait inside a step)
         sync_all()
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        own = elapsed
         P.timing_read()
         samples = np.asarray(P.timing_samples(), dtype=np.float64) * 1e3  # us per main-kernel launch
         P.timing(False)
@@ -259,7 +262,7 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return elapsed, samples
+        return elapsed, samples, own, issue
 
     # Pass 1, one stream, every launch stamped by HIP events: its per-launch
     # kernel durations (dispatch-packet events, non-overlapping) give the
@@ -280,8 +283,9 @@ def main():
     # start/stop: ~5 us of extra gap per launch, measured on C2); the serial
     # and value passes run as a server does, without them.
     samples = timed(1, args.steps, args.warmup, events=True)[1] if not args.no_kernel_events else np.zeros(0)
-    serial_el = timed(1, args.steps, args.warmup)[0]
-    elapsed = serial_el if nstreams == 1 else timed(nstreams, args.steps, args.warmup)[0]
+    serial_el, _, serial_own, serial_issue = timed(1, args.steps, args.warmup)
+    elapsed, _, own_el, issue_s = ((serial_el, None, serial_own, serial_issue) if nstreams == 1 else
+                                   timed(nstreams, args.steps, args.warmup))
     launches = len(samples)
     kernel_ms = float(samples.sum()) / 1e3
 
@@ -374,6 +378,30 @@ def main():
         line["sustained"] = {"seconds": round(sec, 2), "steps": steps_done, "streams": nstreams,
                              "value": round(batch_bytes * steps_done * world * len(shards) / sec / (1 << 30), 2),
                              "unit": "GiB/s"}
+    # The host thread's issue time per step beside the kernel time per step
+    # (VERDICT r4 #3): one thread driving several devices (--single-thread)
+    # is host-bound once issuing a step's launches takes longer than a
+    # device's kernel for it.
+    line["host_issue"] = {"issue_us_per_step": round(serial_issue / args.steps * 1e6, 2),
+                          "launches_per_step": len(shards),
+                          "kernel_us_per_launch": round(avg_kernel_s * 1e6, 2) if launches else None,
+                          "pass": "serial (one stream per shard): wall time of the issue loop / K"}
+    if dist is not None:
+        # per-rank evidence: a straggling GPU or a slow XCD
+        # pairing on one rank shows here, not only in the MAX-over-ranks value
+        mine = {"rank": rank, "host": socket.gethostname(), "device": devids[0],
+                "value": round(batch_bytes * args.steps * len(shards) / own_el / (1 << 30), 2),
+                "serial": round(batch_bytes * args.steps * len(shards) / serial_own / (1 << 30), 2),
+                "avg_launch_us": round(avg_kernel_s * 1e6, 2) if launches else None}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        line["per_rank"] = allr
+        for key, tgt in (("avg_launch_us", line["roofline"]), ("value", line)):
+            vals = [r[key] for r in allr if r[key] is not None]
+            if vals:
+                arg = max(range(len(allr)), key=lambda k: allr[k][key] or 0)
+                tgt[f"{key}_per_rank"] = {"min": min(vals), "max": max(vals), "argmax_rank": allr[arg]["rank"],
+                                          "spread": round(max(vals) / min(vals) - 1, 4)}
     if len(shards) > 1 and dist is None:
         line["shards_checked"], line["buffers_checked"] = shard_parity(shards, offs, sizes, rotate, P)
     if dist is not None:

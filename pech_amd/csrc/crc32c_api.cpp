@@ -297,10 +297,12 @@ static uint64_t flat_tag()
 			fclose(f);
 		g_flat_tag.store(t);
 	});
+	// below 2^62: the kernel keeps two states per tag in the 64-bit word
+	// (tag << 1, tag << 1 | 1); 0 (a zeroed workspace's value) is skipped
 	uint64_t t;
-	while ((t = g_flat_tag.fetch_add(1) + 1) == 0) // (0: a zeroed workspace's value)
+	while (((t = g_flat_tag.fetch_add(1) + 1) & ((1ull << 62) - 1u)) == 0)
 		;
-	return t;
+	return t & ((1ull << 62) - 1u);
 }
 
 // d_dsts != NULL: fused CRC + copy (d_dsts[i] receives descriptor i's bytes)

@@ -47,10 +47,13 @@
 #include <time.h>
 #include <string.h>
 #include <sys/eventfd.h>
+#include <sys/prctl.h>
 #include <unistd.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <deque>
+#include <thread>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -247,6 +250,7 @@ constexpr uint32_t kSlotDescs = 8192;    // descriptors per slot
 constexpr uint32_t kDirectMax = 32u << 10;
 constexpr unsigned kMaxSlots = 4;        // slots in flight per context
 constexpr uint64_t kQueryAfterNs = 1000000; // complete(): a stream is queried once its batch is this old
+constexpr size_t kPollMax = 8u << 20;       // a lone batch of at most this many bytes is polled (notify)
 
 struct Piece {
 	uint64_t item; // submission id
@@ -293,6 +297,8 @@ struct Slot {
 	bool inflight = false;
 	bool queued = false;      // CRC32C_ASYNC_DMA: filled, launched once the slots before it are harvested
 	bool inject_fail = false; // test build: this batch's stream "failed" (PECH_FAULT_ASYNC_STREAM)
+	hipEvent_t ev_done = nullptr; // notifier: recorded after the results' D2H
+	uint64_t est_ns = 0;          // notifier: the batch's expected time (host link rate)
 	uint64_t t_launch = 0;    // mono_ns() at launch
 };
 
@@ -336,6 +342,24 @@ struct crc32c_async {
 	uint64_t prof_ns[5] = {0, 0, 0, 0, 0}; // copies issued, kernels + D2H + host function, waits for a slot, submit, complete
 	uint64_t launches = 0;  // batches launched (crc32c_async_get_stats)
 	uint64_t submitted = 0; // submissions accepted
+	// How a finished batch reaches the eventfd.  A host function on the
+	// slot's stream (hipLaunchHostFunc) sleeps until an interrupt, but the
+	// runtime takes ~10 us to run it: a lone 64 KiB payload waited 37.7 us
+	// p50 for its CRC, 26.7 with the context's notifier thread polling an
+	// event recorded after the results' D2H instead -- which costs that
+	// thread the batch's duration in CPU (profiles/r05/msgr_notify.txt).  So
+	// (3, the default) a batch launched while no other is in flight, of at
+	// most kPollMax bytes, is polled -- after sleeping through most of its
+	// expected time -- and any other by a host function.
+	// PECH_ASYNC_NOTIFY (A/B): 0 = host functions only; 1 = the notifier
+	// blocks in hipEventSynchronize (hipEventBlockingSync; it spun: 100 us
+	// of CPU per 4 MiB payload); 2 = it polls every batch.
+	int notify = 3;
+	std::thread notifier;
+	std::mutex nmu;
+	std::condition_variable ncv;
+	std::deque<Slot *> nq; // launched slots, in launch order
+	bool nstop = false;
 };
 
 static inline uint64_t thread_ns()
@@ -380,6 +404,8 @@ static void slot_free(Slot *s)
 		(void)hipHostFree(s->h_out);
 	if (s->d_out)
 		(void)hipFree(s->d_out);
+	if (s->ev_done)
+		(void)hipEventDestroy(s->ev_done);
 
 	delete s;
 }
@@ -682,8 +708,29 @@ static int issue_slot(crc32c_async *a, Slot *s)
 	// test build: a batch whose stream fails after the launch -- HIP then
 	// skips its host function, so the eventfd stays quiet
 	s->inject_fail = pech_fault(PECH_FAULT_ASYNC_STREAM);
-	if (!s->inject_fail)
-		TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_slot(a, s, -EIO));
+	bool poll = a->notify == 1 || a->notify == 2;
+	if (a->notify == 3) { // a lone, small batch: polled
+		unsigned others = 0;
+		for (const Slot *o : a->inflight)
+			others += o != s && !o->queued;
+		poll = others == 0 && s->used + s->zc_bytes <= kPollMax;
+	}
+	if (!poll) {
+		if (!s->inject_fail)
+			TRY_HIP(hipLaunchHostFunc(s->stream, host_notify, s), fail_slot(a, s, -EIO));
+	} else {
+		s->est_ns = 8000u + (uint64_t)((s->used + s->zc_bytes) / 40u); // (40 bytes/ns: the host link)
+		if (!s->ev_done)
+			TRY_HIP(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming |
+									(a->notify == 1 ? hipEventBlockingSync : 0u)),
+				fail_slot(a, s, -EIO));
+		TRY_HIP(hipEventRecord(s->ev_done, s->stream), fail_slot(a, s, -EIO));
+		{
+			std::lock_guard<std::mutex> lk(a->nmu);
+			a->nq.push_back(s);
+		}
+		a->ncv.notify_one();
+	}
 	s->t_launch = mono_ns();
 	if (s->queued) {
 		s->queued = false; // (already in a->inflight, in order)
@@ -716,6 +763,54 @@ static int launch_slot(crc32c_async *a)
 	return issue_slot(a, s);
 }
 
+// The notifier thread (notify modes 1, 2): waits for each launched slot's
+// event in launch order and does what the host function would (host_notify).
+// A failed batch is left to reap()'s stream query, as with the host function,
+// which HIP skips on a failed stream.
+static void notifier_main(crc32c_async *a)
+{
+	(void)hipSetDevice(a->dev);
+	(void)prctl(PR_SET_TIMERSLACK, 1000ul, 0ul, 0ul, 0ul); // 1 us: the predictive sleep wakes on time
+	for (;;) {
+		Slot *s;
+		{
+			std::unique_lock<std::mutex> lk(a->nmu);
+			a->ncv.wait(lk, [a] { return a->nstop || !a->nq.empty(); });
+			if (a->nq.empty())
+				return; // (stop, nothing left)
+			s = a->nq.front();
+			a->nq.pop_front();
+		}
+		hipError_t e;
+		if (a->notify == 1) {
+			e = hipEventSynchronize(s->ev_done);
+		} else {
+			// sleep through ~70 % of the expected time (this thread's timer
+			// slack is 1 us), then poll; a batch far beyond its estimate (a
+			// slow link, a busy GPU) is polled every 20 us
+			const uint64_t t0 = mono_ns();
+			if (s->est_ns > 30000u) {
+				const uint64_t ns = s->est_ns * 7u / 10u - 10000u;
+				struct timespec ts = {(time_t)(ns / 1000000000u), (long)(ns % 1000000000u)};
+				while (nanosleep(&ts, &ts) && errno == EINTR) {
+				}
+			}
+			while ((e = hipEventQuery(s->ev_done)) == hipErrorNotReady) {
+				if (mono_ns() - t0 > 2 * s->est_ns + 100000u) {
+					struct timespec ts = {0, 20000};
+					nanosleep(&ts, nullptr);
+				} else {
+					__builtin_ia32_pause();
+				}
+			}
+		}
+		if (e == hipSuccess && !s->inject_fail)
+			host_notify(s);
+		else
+			(void)hipGetLastError();
+	}
+}
+
 static struct crc32c_async *async_create(unsigned int flags)
 {
 	if ((flags & ~(CRC32C_ASYNC_ZEROCOPY | CRC32C_ASYNC_DMA)) ||
@@ -742,12 +837,16 @@ static struct crc32c_async *async_create(unsigned int flags)
 	}
 	const char *pf = getenv("PECH_ASYNC_PROF");
 	a->prof = pf && pf[0] == '1';
+	if (const char *nm = getenv("PECH_ASYNC_NOTIFY"))
+		a->notify = nm[0] == '1' ? 1 : nm[0] == '2' ? 2 : 0;
 	a->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
 	if (a->efd < 0) {
 		pech_internal_set_err("crc32c_async_create: eventfd: %s", strerror(errno));
 		crc32c_async_destroy(a);
 		return nullptr;
 	}
+	if (a->notify)
+		a->notifier = std::thread(notifier_main, a);
 	a->ready = true;
 	return a;
 }
@@ -1001,6 +1100,14 @@ extern "C" void crc32c_async_destroy(struct crc32c_async *a)
 		return;
 	if (a->ready)
 		(void)crc32c_async_drain(a); // callbacks on the caller's stack
+	if (a->notifier.joinable()) {
+		{
+			std::lock_guard<std::mutex> lk(a->nmu);
+			a->nstop = true;
+		}
+		a->ncv.notify_one();
+		a->notifier.join();
+	}
 	on_lib_stack([&] {
 		DeviceGuard dg(a->dev >= 0 ? a->dev : 0);
 		for (Slot *s : a->slots)

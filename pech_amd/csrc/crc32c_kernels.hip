@@ -1462,12 +1462,27 @@ __device__ __forceinline__ bool prologue_flat(uint32_t *lds, const u32x4 (&dv)[4
 
 // FLAT (pech_crc32c_flat): the same walk for n <= PECH_FLAT_MAX buffers with
 // no plan kernel -- the descriptors are read at entry (descs) and kept in LDS
-// (prologue_flat), and out[] is zeroed by workgroup 0 and published through
-// *flag = tag (below).
-// Flat batches, workgroup 0's first wave, after its zeroes are published:
-// the seed terms x^(8 len) s of R(s, D) = x^(8|D|) s ^ R(0, D), and the seed
-// itself for an empty buffer, XORed into out[] (the messenger's seeds are 0:
-// nothing to do).
+// (prologue_flat), and out[] is zeroed inside the launch, published through
+// *flag (below).
+//
+// *flag, a word of the caller's workspace, holds FLAT_INIT(tag) while a wave
+// of the launch initialises out[] and FLAT_DONE(tag) once it has; any other
+// value is a previous launch's (or the garbage of a fresh workspace: the host
+// gives every flat launch a fresh tag, below 2^62).  Workgroup 0's first
+// wave claims the job at entry (an exchange); any wave that reaches its first
+// XOR into out[] before FLAT_DONE and finds no claim of this launch claims it
+// itself (a compare-and-swap from the value it read) -- so waves only ever
+// wait for a wave that is running and initialising, never for workgroup 0 to
+// be dispatched.  (Waiting for workgroup 0 deadlocked two concurrent flat
+// launches on one GPU: each one's waiting workgroups held the CUs the other's
+// workgroup 0 needed, until the wait's bound let them go on with out[]
+// uninitialised -- found by test_torchrun_two_ranks_real_kernels.)
+#define FLAT_INIT(tag) ((tag) << 1)
+#define FLAT_DONE(tag) (((tag) << 1) | 1ull)
+
+// Flat batches: the seed terms x^(8 len) s of R(s, D) = x^(8|D|) s ^ R(0, D),
+// and the seed itself for an empty buffer, XORed into out[] by the wave that
+// initialises it (the messenger's seeds are 0: nothing to do).
 __device__ __forceinline__ void flat_seeds(const u32x4 (&dv)[4], uint32_t n, uint32_t lane,
 					   const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
 {
@@ -1479,35 +1494,69 @@ __device__ __forceinline__ void flat_seeds(const u32x4 (&dv)[4], uint32_t n, uin
 	}
 }
 
-// The other waves of a flat launch see out[] zeroed once *flag holds this
-// launch's tag.  Their early load (issued just before the ring's prime and
-// consumed behind it, so it costs no wait) normally already returns it, and
-// `ready` is set then; otherwise this polls, once per wave, before its
-// first XOR into out[].  No acquire fence: every access to out[] in the
-// launch is a device-scope atomic (the zeroes too), ordered at the word
-// itself, and the XORs are issued only after the tag was read.  (An acquire
-// here was an L2 invalidate per wave: +6.5 us per C3 launch.)
-__device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &ready)
+// The claimed job: zeroes (device-scope atomic exchanges: every access to
+// out[] in the launch is a device-scope atomic, ordered at the word itself),
+// the seed terms after them, then FLAT_DONE (a release store).  No acquire on
+// the readers' side: they only XOR, after they read FLAT_DONE.  (An acquire
+// there was an L2 invalidate per wave: +6.5 us per C3 launch.)
+// (The descriptors are read again here, in this rare path, when there are
+// seeds: kept in registers for it, they pushed the kernel past 128 VGPRs.)
+__device__ __forceinline__ void flat_init(const pech_desc *__restrict__ descs, uint32_t n, uint32_t lane,
+					  const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint64_t *flag,
+					  uint64_t tag, bool seeds)
+{
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k)
+		if (4u * lane + k < n)
+			(void)atomicExch(out + 4u * lane + k, 0u);
+	if (seeds) {
+		u32x4 dv[4];
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k)
+			dv[k] = ((const u32x4 *)descs)[min(4u * lane + k, n - 1u)];
+		__threadfence(); // the zeroes are performed before the seed terms land on the same words
+		flat_seeds(dv, n, lane, consts, out);
+	}
+	if (lane == 0)
+		__hip_atomic_store(flag, FLAT_DONE(tag), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Before a wave's first XOR into out[]: `ready` once it has read FLAT_DONE
+// (normally from its early load, issued with the ring's prime and looked at
+// behind the tables' barrier, so it costs no wait); otherwise poll -- and
+// claim the job when no wave of this launch has (see above).  Each poll is
+// consumed before the loop can exit, so no load of this rare path is left
+// pending at the step loop's join, where the compiler would wait for it with
+// a vmcnt(0), i.e. drain the ring at every step end.  (Bounded: a wave never
+// waits forever; ~1 s, then it goes on, and the bounds-checked build says so.)
+__device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &ready,
+					   const pech_desc *__restrict__ descs, uint32_t n, uint32_t lane,
+					   const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, bool seeds)
 {
 	if (ready)
 		return;
-	// (bounded: a wave never waits forever -- ~1 s, then it goes on, and the
-	// bounds-checked build reports it; workgroup 0 is dispatched before any
-	// workgroup of its XCD, so in practice the tag is there within
-	// microseconds).  Each poll is consumed before the loop can exit, so no
-	// load of this rare path is left pending at the step loop's join, where
-	// the compiler would wait for it with a vmcnt(0) -- a drain of the ring
-	// at every step end.
 	for (uint32_t spin = 0;; ++spin) {
 		const uint64_t v = uni64(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-		if (v == tag || spin >= (1u << 24)) {
+		if (v == FLAT_DONE(tag))
+			break;
+		if ((v >> 1) != tag) { // no claim of this launch: claim it
+			uint64_t got = 0;
+			if (lane == 0)
+				got = atomicCAS((unsigned long long *)flag, (unsigned long long)v, (unsigned long long)FLAT_INIT(tag));
+			if (uni64(got) == v) {
+				flat_init(descs, n, lane, consts, out, flag, tag, seeds);
+				break;
+			}
+			continue; // another wave claimed it first
+		}
+		if (spin >= (1u << 24)) {
 #ifdef PECH_DEBUG_BOUNDS
-			if (v != tag && (threadIdx.x & 63u) == 0)
-				printf("PECH OOB flat tag never published blk %u\n", blockIdx.x);
+			if (lane == 0)
+				printf("PECH OOB flat out[] never initialised blk %u\n", blockIdx.x);
 #endif
 			break;
 		}
-		__builtin_amdgcn_s_sleep(2);
+		__builtin_amdgcn_s_sleep(2); // FLAT_INIT: a running wave is at it
 	}
 	ready = true;
 }
@@ -1535,23 +1584,14 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const uint32_t wave = uni(tid >> 6);
 	const uint32_t W = gridDim.x * PECH_MAIN_WAVES;
 	const uint32_t nchunks = (n + PECH_CHUNK - 1u) / PECH_CHUNK;
+	// Flat: workgroup 0's first wave claims the initialisation of out[] first
+	// thing (an exchange; its result is looked at once the descriptors are
+	// in, which the seed terms need); see flat_init
+	uint64_t claim0 = 0;
+	bool seeds = false; // flat: some buffer of the batch has a seed
 	if constexpr (FLAT) {
-		// Workgroup 0's first wave zeroes out[] and publishes it, first thing:
-		// *flag = tag, a release store at device scope once the zeroes are
-		// done (atomic exchanges: every access to out[] in the launch is a
-		// device-scope atomic).  The other waves XOR their runs into out[]
-		// only once they have seen the tag (flat_ready), so no plan kernel
-		// has to initialise out[].  The host gives every flat launch a fresh
-		// 64-bit tag; graph captures, whose replays would repeat it, take the
-		// planned path.
-		if (blockIdx.x == 0 && wave == 0) {
-#pragma unroll
-			for (uint32_t k = 0; k < 4; ++k)
-				if (4u * lane + k < n)
-					(void)atomicExch(out + 4u * lane + k, 0u);
-			if (lane == 0)
-				__hip_atomic_store(flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-		}
+		if (blockIdx.x == 0 && wave == 0 && lane == 0)
+			claim0 = atomicExch((unsigned long long *)flag, (unsigned long long)FLAT_INIT(tag));
 	}
 
 	// Prologue (v0.11): three dependent global rounds before the first data
@@ -1685,8 +1725,18 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	if constexpr (FLAT) {
 		uint32_t Rtot;
 		live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot);
-		if (blockIdx.x == 0 && wave == 0)
-			flat_seeds(dv, n, lane, consts, out);
+		seeds = __ballot((4u * lane < n && dv[0].w) || (4u * lane + 1u < n && dv[1].w) ||
+				 (4u * lane + 2u < n && dv[2].w) || (4u * lane + 3u < n && dv[3].w)) != 0ull;
+		if (blockIdx.x == 0 && wave == 0) {
+			// (lane 0's exchange: a claim of this launch already there -- another
+			// wave got in first -- leaves the job to it; a FLAT_DONE it
+			// overwrote goes back)
+			const uint64_t c0 = lane_value((uint32_t)claim0, 0) | (uint64_t)lane_value((uint32_t)(claim0 >> 32), 0) << 32;
+			if ((c0 >> 1) != tag)
+				flat_init(descs, n, lane, consts, out, flag, tag, seeds);
+			else if (c0 == FLAT_DONE(tag) && lane == 0)
+				__hip_atomic_store(flag, FLAT_DONE(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
 		if (!live)
 			return; // whole workgroup idle (small batch)
 		early_fill = !PECH_IL_CRC && Rtot <= (uint64_t)PECH_EARLY_FILL_ROWS * gridDim.x; // workgroup-uniform
@@ -1777,7 +1827,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// barrier below); every other wave reads the flag now, just before its
 	// prime, and looks at it behind the tables' fill and barrier (below)
 	uint64_t seen = 0;
-	bool ready = !FLAT || blockIdx.x == 0;
+	bool ready = !FLAT;
 	if constexpr (FLAT) {
 		// Unconditional, as one block: the flag's wait below then counts the
 		// prime's loads after it (vmcnt(7)) and no ring copy joins a path
@@ -1809,7 +1859,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// (looked at only now, the flag's round trip hides behind the fill and
 	// the barrier)
 	if (FLAT && S.T)
-		ready = ready || uni64(seen) == tag;
+		ready = ready || uni64(seen) == FLAT_DONE(tag);
 	STAMP(t_start);
 	// the wave's first pool claim, one item ahead (resolved when its first
 	// item is done)
@@ -2005,7 +2055,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		tq[2] = __builtin_amdgcn_s_memrealtime();
 #endif
 		if (FLAT)
-			flat_ready(flag, tag, ready);
+			flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds);
 		finish_run<!COPY>(lds, g8, s0, s1, s2, s3, step_m<FLAT>(S), STEP_RA(S), tpow, S.nu != 0, out, step_orig<FLAT>(S));
 		tpow = tpow_n;
 #ifdef PECH_STAMP_FIN
@@ -2030,7 +2080,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		static_assert(PECH_DEFER_SLOTS == 64u, "one slot per lane of the flushing wave");
 		if (done == PECH_MAIN_WAVES - 1u) {
 			if (FLAT)
-				flat_ready(flag, tag, ready);
+				flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds);
 			const uint32_t k = lds[L_DEFER / 4u + lane];
 			bool flush = k != PECH_DEFER_EMPTY;
 #ifdef PECH_DEBUG_BOUNDS

@@ -57,6 +57,15 @@ def test_torchrun_two_ranks_real_kernels():
     assert d["shards_checked"] == 2 and d["buffers_checked"] == 2 * d["config"]["buffers_per_gpu"] * 2
     assert d["config"]["parallelism"].startswith("shard2")
     assert "cpu_baseline" not in d  # rank 0 at N=1 only
+    # per-rank evidence: every rank's own rate and launch
+    # time, and which rank is slowest
+    pr = d["per_rank"]
+    assert sorted(r["rank"] for r in pr) == [0, 1] and all(r["value"] > 0 and r["avg_launch_us"] > 0 for r in pr)
+    a = d["roofline"]["avg_launch_us_per_rank"]
+    assert a["min"] <= a["max"] and a["argmax_rank"] in (0, 1)
+    assert a["max"] == max(r["avg_launch_us"] for r in pr)
+    v = d["value_per_rank"]
+    assert v["min"] == min(r["value"] for r in pr) and v["max"] == max(r["value"] for r in pr)
 
 
 def test_torchrun_rccl_process_group_one_rank():
@@ -86,3 +95,6 @@ def test_single_thread_eight_shards_on_one_gpu():
     assert d["shards_checked"] == 8 and d["n_gpus"] == 1
     assert d["buffers_checked"] == 8 * d["config"]["buffers_per_gpu"] * 2
     assert d["value"] > 0
+    # the one thread's issue time per step of 8 launches, beside the kernel time
+    h = d["host_issue"]
+    assert h["launches_per_step"] == 8 and h["issue_us_per_step"] > 0 and h["kernel_us_per_launch"] > 0

@@ -4,10 +4,11 @@ oracle, bit-exact, and against the two-launch plan + main path on the same
 batch.  Cases particular to this kernel: its rows cover ALL of a buffer's
 bytes (last-line pieces kept below kb bytes, x^(-8T) at the end), empty
 buffers kept in place in descriptor order (runs of them before large ones),
-seeds added by workgroup 0, out[] zeroed in the launch and published by a
-per-launch tag (garbage in out[], back-to-back launches on one workspace,
-two workspaces on two streams), the uniform pool, one buffer split over
-many workgroups, and the 256 / 257 boundary to the planned path."""
+seeds added by the wave that initialises out[], out[] zeroed in the launch
+and published by a per-launch tag (garbage in out[], back-to-back launches
+on one workspace, two and four streams at once, whose workgroups interleave
+on the CUs), the uniform pool, one buffer split over many workgroups, and
+the 256 / 257 boundary to the planned path."""
 import numpy as np
 import pytest
 
@@ -216,3 +217,32 @@ def test_flat_and_planned_agree_on_c3(torch_dev, P):
 def test_set_flat_max_clamps(P):
     prev = P.set_flat_max(10 ** 6)
     assert P.set_flat_max(prev) == FLAT_MAX
+
+
+def test_concurrent_flat_launches_on_four_streams(torch_dev, P):
+    """Flat launches on four streams at once, each large enough to fill the
+    chip: their workgroups interleave on the CUs, so one launch's workgroup 0
+    may wait for a CU while its other workgroups reach their first XOR.
+    Those may not wait for workgroup 0 (two such launches deadlocked each
+    other, each holding the CUs the other's workgroup 0 needed): a running
+    wave claims out[]'s initialisation instead (flat_init)."""
+    torch, dev = torch_dev
+    streams = [torch.cuda.Stream(device=dev) for _ in range(4)]
+    wss = [torch.empty(P.workspace_bytes(FLAT_MAX), dtype=torch.uint8, device=dev) for _ in range(8)]
+    rng = np.random.default_rng(44)
+    n, L = 128, 1 << 20
+    bufs = [rand_buf(torch, dev, n * L + 64, 500 + k) for k in range(4)]
+    torch.cuda.synchronize()
+    jobs = []
+    for k in range(32):
+        off = np.sort(rng.integers(0, 64, n)) + np.arange(n, dtype=np.int64) * L
+        lens = rng.integers(L // 2, L - 64, n)
+        seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64) if k % 3 == 0 else None
+        b = bufs[k % 4]
+        out, descs = dev_crcs(torch, P, b, off, lens, seeds, ws=wss[k % 8], stream=streams[k % 4], sync=False)
+        jobs.append((b, off, lens, seeds, out, descs))
+    torch.cuda.synchronize()
+    hosts = [b.cpu().numpy() for b in bufs]
+    for k, (b, off, lens, seeds, out, _) in enumerate(jobs):
+        want = O.crcs(hosts[k % 4], off, lens, seeds)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), k
