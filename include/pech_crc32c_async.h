@@ -146,6 +146,8 @@ struct crc32c_async_stats {
 	uint64_t launches;      /* batches launched                               */
 	unsigned int inflight;  /* batches launched and not yet harvested         */
 	unsigned int queued;    /* CRC32C_ASYNC_DMA: filled slots waiting to launch */
+	uint64_t host_out;      /* launches whose kernel stored the results in host memory itself */
+	uint64_t polled;        /* launches whose completion the context's thread polled */
 };
 int crc32c_async_get_stats(const struct crc32c_async *a, struct crc32c_async_stats *st);
 

@@ -32,7 +32,8 @@ class CStats(ctypes.Structure):
 class CAsyncStats(ctypes.Structure):
     """struct crc32c_async_stats (include/pech_crc32c_async.h)."""
     _fields_ = [("device", ctypes.c_int), ("submitted", ctypes.c_uint64), ("launches", ctypes.c_uint64),
-                ("inflight", ctypes.c_uint), ("queued", ctypes.c_uint)]
+                ("inflight", ctypes.c_uint), ("queued", ctypes.c_uint), ("host_out", ctypes.c_uint64),
+                ("polled", ctypes.c_uint64)]
 
 
 # completion callback of include/pech_crc32c_async.h: (arg, crc, err)

@@ -322,7 +322,7 @@ class AsyncCrc:
 
     def stats(self):
         """crc32c_async_get_stats as a dict (device, submitted, launches,
-        inflight, queued)."""
+        inflight, queued, host_out, polled)."""
         from ._lib import CAsyncStats
 
         st = CAsyncStats()

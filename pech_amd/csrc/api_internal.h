@@ -11,10 +11,14 @@
 
 #define PECH_HIDDEN __attribute__((visibility("hidden")))
 
-// plan + main kernels for n device descriptors on `stream`, explicit
-// workspace (pech_ws_bytes(n) bytes, 256-byte aligned); current device
+// The kernels for n device descriptors on `stream` (small: the direct
+// kernel; else flat, or plan + main), explicit workspace (pech_ws_bytes(n)
+// bytes, 256-byte aligned); current device.  hout (a device-visible pinned
+// host array of n words, or NULL): returns 1 when the results are stored
+// there by the kernel itself, 0 when they are in d_out (the caller copies),
+// a negative errno on failure.
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-				     size_t ws_bytes, hipStream_t stream, bool small = false);
+				     size_t ws_bytes, hipStream_t stream, bool small = false, uint32_t *hout = nullptr);
 // The GPUs a multi-device caller spreads over: PECH_DEVICES="0,0,..." (a
 // repeated id puts several shards or contexts on one GPU: how one-GPU boxes
 // rehearse eight) or every visible device.  Count, or a negative errno.

@@ -43,7 +43,7 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *, uint32_t, const uint
 extern "C" hipError_t pech_launch_small(const void *, uint32_t, uint32_t, const uint32_t *, uint32_t *, uint32_t,
 					hipStream_t);
 extern "C" hipError_t pech_launch_flat(const pech_desc *, uint32_t, const uint32_t *, uint32_t *, uint32_t, uint32_t,
-				       uint64_t *, uint64_t, hipStream_t, hipEvent_t, hipEvent_t);
+				       uint64_t *, uint64_t, hipStream_t, hipEvent_t, hipEvent_t, uint32_t *);
 
 // ---------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -305,9 +305,12 @@ static uint64_t flat_tag()
 	return t & ((1ull << 62) - 1u);
 }
 
-// d_dsts != NULL: fused CRC + copy (d_dsts[i] receives descriptor i's bytes)
+// d_dsts != NULL: fused CRC + copy (d_dsts[i] receives descriptor i's bytes).
+// hout != NULL (the async layer's slots): a flat launch also stores the
+// results there, a device-visible pinned host array (*published = true).
 static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-			size_t ws_bytes, hipStream_t stream, const uint64_t *d_dsts = nullptr)
+			size_t ws_bytes, hipStream_t stream, const uint64_t *d_dsts = nullptr, uint32_t *hout = nullptr,
+			bool *published = nullptr)
 {
 	if (n == 0)
 		return 0;
@@ -337,8 +340,13 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			}
 		}
 		if (flat)
+		{
+			const bool pub = hout && m == n; // (one launch: a flat batch is)
 			HIP_TRY(pech_launch_flat(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, rpw_min(),
-						 (uint64_t *)ws, flat_tag(), stream, tl.a, tl.b));
+						 (uint64_t *)ws, flat_tag(), stream, tl.a, tl.b, pub ? hout : nullptr));
+			if (pub && published)
+				*published = true;
+		}
 		else
 			HIP_TRY(pech_launch_main(m, &w, c->d_consts, d_out + off, (uint32_t)c->ncu, rpw_min(),
 						 d_dsts != nullptr, stream, tl.a, tl.b));
@@ -405,14 +413,19 @@ static int launch_small(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 // internal entry points for crc32c_async.cpp (hidden: not part of the C-ABI)
 
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-				     size_t ws_bytes, hipStream_t stream, bool small)
+				     size_t ws_bytes, hipStream_t stream, bool small, uint32_t *hout)
 {
 	std::lock_guard<std::mutex> lk(g_mu);
 	DevCtx *c = nullptr;
 	int rc = ctx_get(&c);
 	if (rc)
 		return rc;
-	return small ? launch_small(c, d_descs, d_out, n, stream) : launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream);
+	if (small) // the direct kernel stores each result once: straight to the host array when there is one
+		return hout && n <= PECH_MAX_BATCH ? (launch_small(c, d_descs, hout, n, stream) ?: 1)
+						   : launch_small(c, d_descs, d_out, n, stream);
+	bool pub = false;
+	rc = launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream, nullptr, hout, &pub);
+	return rc ? rc : pub ? 1 : 0;
 }
 
 PECH_HIDDEN int pech_internal_device_list(int *devs, int max, int max_per_dev)

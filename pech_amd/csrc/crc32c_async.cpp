@@ -285,6 +285,7 @@ struct Slot {
 	pech_desc *h_desc = nullptr, *d_desc = nullptr;
 	const pech_desc *desc_view = nullptr; // device mapping of h_desc: the plan kernel reads it in place
 	uint32_t *h_out = nullptr, *d_out = nullptr;
+	uint32_t *out_view = nullptr; // device mapping of h_out: flat and direct launches store the results there
 	std::atomic<int> finished{0}; // set by the stream's host function after the results' D2H
 	std::atomic<int> waiting{0};  // a submit sleeps on `finished` (futex): the host function wakes it
 	int efd = -1;                 // the context's eventfd
@@ -342,6 +343,8 @@ struct crc32c_async {
 	uint64_t prof_ns[5] = {0, 0, 0, 0, 0}; // copies issued, kernels + D2H + host function, waits for a slot, submit, complete
 	uint64_t launches = 0;  // batches launched (crc32c_async_get_stats)
 	uint64_t submitted = 0; // submissions accepted
+	uint64_t host_out = 0;  // launches whose results the kernel stored in h_out
+	uint64_t polled = 0;    // launches notified by the notifier thread
 	// How a finished batch reaches the eventfd.  A host function on the
 	// slot's stream (hipLaunchHostFunc) sleeps until an interrupt, but the
 	// runtime takes ~10 us to run it: a lone 64 KiB payload waited 37.7 us
@@ -432,6 +435,12 @@ static Slot *slot_new(int efd)
 		s->desc_view = (const pech_desc *)dv;
 	else
 		(void)hipGetLastError(); // no mapping: descriptors go by H2D copy
+	const char *ho = getenv("PECH_ASYNC_HOST_OUT"); // A/B: 0 = results by D2H copy after every launch
+	dv = nullptr;
+	if (!(ho && ho[0] == '0') && hipHostGetDevicePointer(&dv, s->h_out, 0) == hipSuccess && dv)
+		s->out_view = (uint32_t *)dv;
+	else
+		(void)hipGetLastError();
 	return s;
 }
 
@@ -700,11 +709,18 @@ static int issue_slot(crc32c_async *a, Slot *s)
 		pech_internal_set_err("crc32c_async: injected launch failure (test)");
 		return fail_slot(a, s, -EIO);
 	}
+	// results: stored into h_out by the flat and direct kernels themselves
+	// (rc 1: no copy after them -- a blit kernel and its dispatch, ~4-5 us of
+	// a lone payload's latency, profiles/r05/lat_prof.txt), else copied
 	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream,
-				      s->maxlen < kDirectMax && !a->planned_only);
-	if (rc)
+				      s->maxlen < kDirectMax && !a->planned_only, s->out_view);
+	if (rc < 0)
 		return fail_slot(a, s, rc);
-	TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream), fail_slot(a, s, -EIO));
+	if (rc == 0)
+		TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream),
+			fail_slot(a, s, -EIO));
+	else
+		a->host_out++;
 	// test build: a batch whose stream fails after the launch -- HIP then
 	// skips its host function, so the eventfd stays quiet
 	s->inject_fail = pech_fault(PECH_FAULT_ASYNC_STREAM);
@@ -729,6 +745,7 @@ static int issue_slot(crc32c_async *a, Slot *s)
 			std::lock_guard<std::mutex> lk(a->nmu);
 			a->nq.push_back(s);
 		}
+		a->polled++;
 		a->ncv.notify_one();
 	}
 	s->t_launch = mono_ns();
@@ -838,7 +855,7 @@ static struct crc32c_async *async_create(unsigned int flags)
 	const char *pf = getenv("PECH_ASYNC_PROF");
 	a->prof = pf && pf[0] == '1';
 	if (const char *nm = getenv("PECH_ASYNC_NOTIFY"))
-		a->notify = nm[0] == '1' ? 1 : nm[0] == '2' ? 2 : 0;
+		a->notify = nm[0] >= '0' && nm[0] <= '3' ? nm[0] - '0' : 3;
 	a->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
 	if (a->efd < 0) {
 		pech_internal_set_err("crc32c_async_create: eventfd: %s", strerror(errno));
@@ -900,6 +917,8 @@ extern "C" int crc32c_async_get_stats(const struct crc32c_async *a, struct crc32
 	st->device = a->dev;
 	st->submitted = a->submitted;
 	st->launches = a->launches;
+	st->host_out = a->host_out;
+	st->polled = a->polled;
 	st->inflight = st->queued = 0;
 	for (const Slot *s : a->inflight)
 		(s->queued ? st->queued : st->inflight)++;

@@ -1117,10 +1117,45 @@ __device__ __forceinline__ uint32_t share_head(uint32_t a, uint32_t b)
 	return min(b, max(a + PECH_ITEM_ROWS, b - min(PECH_POOL_ROWS, b - a)));
 }
 
+// Wave priority (s_setprio) from a static share's progress: 3 while more
+// than 3/4 of the share's rows remain, then 2, 1, 0.  The SQ issues
+// oldest-first among waves of equal priority, so with equal static shares a
+// CU's four waves per SIMD finished in age order, up to 65 us apart (C4,
+// busy p50 85 / 108 / 134 / 149 us by age slot, profiles/r05/stamps_c4.txt),
+// and the CU's last quarter ran on a quarter of its waves.  Raising the
+// waves that are behind keeps a CU's waves within about a quarter of a share
+// of each other.  (Pooled and interleaved walks balance otherwise.)
+#ifndef PECH_PRIO_MIN_SHARE
+#define PECH_PRIO_MIN_SHARE 1024u
+#endif
+struct Prio {
+	uint32_t th1, th2, th3, cur;
+};
+__device__ __forceinline__ Prio prio_init(uint32_t tot)
+{
+	return Prio{tot / 4u, tot / 2u, tot - tot / 4u, 0xFFu};
+}
+__device__ __forceinline__ void prio_update(Prio &P, uint32_t rem_rows)
+{
+	const uint32_t q = (rem_rows > P.th1 ? 1u : 0u) + (rem_rows > P.th2 ? 1u : 0u) + (rem_rows > P.th3 ? 1u : 0u);
+	if (q == P.cur)
+		return;
+	P.cur = q;
+	if (q == 3u)
+		__builtin_amdgcn_s_setprio(3);
+	else if (q == 2u)
+		__builtin_amdgcn_s_setprio(2);
+	else if (q == 1u)
+		__builtin_amdgcn_s_setprio(1);
+	else
+		__builtin_amdgcn_s_setprio(0);
+}
+
 // What a main-kernel wave knows after the chunk scan and the start search
 // (prologue_start): all wave-uniform.
 struct Start {
 	uint32_t U0, wg_rows, r0, r1, jmax, rem_all, p0, lr0, jj, pjj, nzjj, nsjj;
+	uint32_t nlive; // live workgroups of the launch (the same in every one)
 	uint64_t wg0;
 	bool uniform, il;
 #ifdef PECH_STAMPS
@@ -1168,6 +1203,7 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 	// VALU work (prologue, fold, shift), and a 4 MiB launch's youngest waves
 	// ended 3.5 us after its oldest (profiles/r05/stamps_flat_v29a.txt).  (Not
 	// with interleaved rows: they walk the workgroup's range together.)
+	st.nlive = prop ? gridDim.x : (uint32_t)min((uint64_t)gridDim.x, ((uint64_t)Rtot + rpw - 1u) / rpw);
 	if (!prop && !il) {
 		const uint64_t k = (uint64_t)wave * gridDim.x + blockIdx.x;
 		if ((uint64_t)blockIdx.x * rpw >= Rtot)
@@ -1184,6 +1220,10 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 		st.il = il;
 		return true;
 	}
+#endif
+#ifdef PECH_WG_MAJOR_SMALL
+	if (!prop)
+		st.nlive = (uint32_t)min((uint64_t)gridDim.x, ((uint64_t)Rtot + PECH_MAIN_WAVES * rpw - 1u) / (PECH_MAIN_WAVES * rpw));
 #endif
 	if (wg0 >= Rtot)
 		return false; // whole workgroup idle (small batch)
@@ -1517,8 +1557,10 @@ __device__ __forceinline__ void flat_init(const pech_desc *__restrict__ descs, u
 		__threadfence(); // the zeroes are performed before the seed terms land on the same words
 		flat_seeds(dv, n, lane, consts, out);
 	}
-	if (lane == 0)
+	if (lane == 0) {
+		(void)atomicExch((uint32_t *)(flag + 1), 0u); // the publication count (flat_publish)
 		__hip_atomic_store(flag, FLAT_DONE(tag), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+	}
 }
 
 // Before a wave's first XOR into out[]: `ready` once it has read FLAT_DONE
@@ -1561,13 +1603,49 @@ __device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &r
 	ready = true;
 }
 
+// Flat launches for the async layer (hout != NULL): the results go to the
+// slot's pinned host array from the kernel itself, instead of a copy after
+// it (a blit kernel, 4.2-4.4 us per lone payload on the stream, plus its
+// dispatch; profiles/r05/lat_prof.txt).  Each live workgroup's last wave,
+// once every XOR of its workgroup is performed, counts itself in (flag + 1);
+// the last of the nlive reads out[] at L2 and stores it to hout.  (The count
+// is zeroed by flat_init, before FLAT_DONE, and a workgroup counts only
+// after it has read FLAT_DONE.)  "Performed": each wave waits for its own
+// atomics' acknowledgements (vm_done) before the workgroup's LDS count --
+// device-scope atomics are performed at L2, where every later atomic and
+// L2 load sees them.  An agent-scope release fence would do it too, but it
+// writes L2 back (buffer_wbl2) in every wave: lone 1 MiB payloads 48 -> 86 us.
+__device__ __forceinline__ void vm_done()
+{
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void flat_publish(uint64_t *flag, uint32_t nlive, uint32_t n, uint32_t lane,
+					     uint32_t *__restrict__ out, uint32_t *__restrict__ hout)
+{
+	vm_done(); // (the flush's XORs; or, with nlive 0, flat_init's zeroes and seeds)
+	if (nlive) { // (0: a launch without rows, published by the wave that initialised out[])
+		uint32_t c = 0;
+		if (lane == 0)
+			c = atomicAdd((uint32_t *)(flag + 1), 1u);
+		if (uni(c) + 1u != nlive)
+			return;
+	}
+	asm volatile("" ::: "memory");
+#pragma unroll
+	for (uint32_t k = 0; k < PECH_FLAT_MAX / 64u; ++k) {
+		const uint32_t p = 64u * k + lane;
+		if (p < n)
+			hout[p] = __hip_atomic_load(out + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+
 template <bool COPY, uint32_t U, bool FLAT = false>
 __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
 					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
 					  const uint32_t *__restrict__ nzs, uint32_t n,
 					  const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min,
 					  const int64_t *__restrict__ deltas, const pech_desc *__restrict__ descs = nullptr,
-					  uint64_t *flag = nullptr, uint64_t tag = 0)
+					  uint64_t *flag = nullptr, uint64_t tag = 0, uint32_t *__restrict__ hout = nullptr)
 {
 	static_assert(!(FLAT && COPY), "flat batches: CRC only");
 	const uint32_t tid = threadIdx.x;
@@ -1737,6 +1815,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			else if (c0 == FLAT_DONE(tag) && lane == 0)
 				__hip_atomic_store(flag, FLAT_DONE(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
+		if (hout && Rtot == 0u && blockIdx.x == 0 && wave == 0) // no rows at all: out[] holds the seeds (flat_init above)
+			flat_publish(flag, 0u, n, lane, out, hout);
 		if (!live)
 			return; // whole workgroup idle (small batch)
 		early_fill = !PECH_IL_CRC && Rtot <= (uint64_t)PECH_EARLY_FILL_ROWS * gridDim.x; // workgroup-uniform
@@ -1873,7 +1953,17 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	uint64_t tq[3] = {0, 0, 0};
 	uint32_t nstep = 0;
 #endif
+#ifdef PECH_NO_PRIO // A/B: every wave at the default priority
+	constexpr bool prio_on = false;
+#else
+	// wave-uniform: static shares of at least PECH_PRIO_MIN_SHARE rows (256 MiB
+	// launches, 512-row shares, lost 2 % with it: profiles/r05/ab_prio.txt)
+	const bool prio_on = !COPY && jmax == 0u && !il && rem_all >= PECH_PRIO_MIN_SHARE;
+#endif
+	Prio prio = prio_init(rem_all);
 	while (S.T) {
+		if (prio_on)
+			prio_update(prio, S.rem + 8u * S.T);
 		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 		// row 0's bytes before the buffer are zeros (free: leading zeros):
 		// zoff -> the whole piece, zh -> its first zh bytes; on 64-bit halves
@@ -1890,6 +1980,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// full blocks: every lane's rows valid, prefetch stays inside every run
 		for (; blk + 1 < nblk && (blk + 2) * U <= S.nmin; ++blk) {
 			const uint64_t base = S.ad + (uint64_t)blk * U * rsb;
+			if (prio_on && blk)
+				prio_update(prio, S.rem + 8u * (S.T - blk * U));
 #if defined(PECH_STAMPS) && !defined(PECH_STAMP_FIN)
 			if (nstep == 0 && (blk == nblk / 4u || blk == nblk / 2u || blk == 3u * nblk / 4u))
 				tq[blk == nblk / 4u ? 0 : (blk == nblk / 2u ? 1 : 2)] = __builtin_amdgcn_s_memrealtime();
@@ -2072,6 +2164,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// earlier wave's table updates precede its count.
 	{
 		uint32_t done = 0;
+		if (FLAT && hout) // this wave's XORs into out[] performed before the workgroup's count (flat_publish)
+			vm_done();
 		__threadfence_block(); // table updates before the count (compiler and LDS order)
 		if (lane == 0)
 			done = atomicAdd(lds + L_DEFER_DONE / 4u, 1u);
@@ -2091,6 +2185,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #endif
 			if (flush)
 				atomicXor(out + k, lds[L_DEFER / 4u + PECH_DEFER_SLOTS + lane]);
+			if (FLAT && hout)
+				flat_publish(flag, sv.nlive, n, lane, out, hout);
 		}
 	}
 #ifdef PECH_STAMPS
@@ -2144,11 +2240,11 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 // `tag` publish workgroup 0's zeroed out[] to the other workgroups.
 extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_flat(
 	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
-	uint32_t rpw_min, uint64_t *__restrict__ flag, uint64_t tag)
+	uint32_t rpw_min, uint64_t *__restrict__ flag, uint64_t tag, uint32_t *__restrict__ hout)
 {
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	main_body<false, PECH_U, true>(lds, nullptr, nullptr, nullptr, nullptr, n, consts, out, rpw_min, nullptr, descs, flag,
-				       tag);
+				       tag, hout);
 }
 
 // ---- direct kernel: small-buffer batches without a plan kernel -------------
@@ -2578,12 +2674,12 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 // pech_launch_main; flag: 8-byte aligned device word, tag: fresh per launch
 extern "C" hipError_t pech_launch_flat(const pech_desc *descs, uint32_t n, const uint32_t *consts, uint32_t *out,
 				       uint32_t ncu, uint32_t rpw_min, uint64_t *flag, uint64_t tag, hipStream_t stream,
-				       hipEvent_t ev_start, hipEvent_t ev_stop)
+				       hipEvent_t ev_start, hipEvent_t ev_stop, uint32_t *hout)
 {
 	if (n == 0 || n > PECH_FLAT_MAX || ((uintptr_t)flag & 7u))
 		return hipErrorInvalidValue;
 	hipExtLaunchKernelGGL(pech_crc32c_flat, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u, descs,
-			      n, consts, out, rpw_min, flag, tag);
+			      n, consts, out, rpw_min, flag, tag, hout);
 	return hipGetLastError();
 }
 
@@ -2606,6 +2702,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.29 gfx950 rows128 wave-steps(8x8-lane groups) grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.30 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -173,6 +173,55 @@ def test_async_context_per_device(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("host_out", ["1", "0"])
+def test_async_results_stored_by_the_kernel(monkeypatch, host_out):
+    """Flat and direct launches store a slot's results in its pinned host
+    array themselves (no copy after the kernel; PECH_ASYNC_HOST_OUT=0 keeps
+    the copy, as planned batches of more than 256 pieces always do), and a
+    lone small batch is polled by the context's thread.  Lone payloads one at
+    a time: 64 KiB and 1 MiB (flat), 4 KiB and 20 KiB pieces (direct), with
+    and without seeds, a zero-length one; then one slot of 300 x 40 KiB
+    (plan + main)."""
+    import pech_amd as P
+
+    monkeypatch.setenv("PECH_ASYNC_HOST_OUT", host_out)
+    rng = np.random.default_rng(12)
+    ac = P.AsyncCrc()
+    got, want, keep = {}, {}, []
+    sizes = [65536, 1 << 20, 4096, 20000, 0, 65536 + 3, 777]
+    k = 0
+    for rep in range(3):
+        for L in sizes:
+            b = rng.integers(0, 256, L, dtype=np.uint8)
+            seed = int(rng.integers(0, 1 << 32)) if k % 2 else 0
+            keep.append(b)
+            want[k] = O.crc(seed, b)
+            ac.submit(b.ctypes.data, L, seed, lambda crc, err, k=k: got.__setitem__(k, (crc, err)), keep=b)
+            ac.drain()  # one batch in flight at a time: a lone batch
+            k += 1
+    st = ac.stats()
+    assert got == {i: (want[i], 0) for i in range(k)}
+    lone = st["launches"]
+    assert lone >= 3 * (len(sizes) - 1), st
+    assert st["polled"] == lone, st  # every lone batch of <= 8 MiB polled
+    assert st["host_out"] == (lone if host_out == "1" else 0), st
+    # more than 256 pieces in one slot: plan + main, results copied
+    base = dict(got)
+    for i in range(300):
+        b = rng.integers(0, 256, 40000, dtype=np.uint8)
+        keep.append(b)
+        want[k] = O.crc(i, b)
+        ac.submit(b.ctypes.data, b.size, i, lambda crc, err, k=k: got.__setitem__(k, (crc, err)), keep=b)
+        k += 1
+    ac.drain()
+    assert got == {i: (want[i], 0) for i in range(k)}
+    st2 = ac.stats()
+    assert st2["launches"] > lone and st2["host_out"] - st["host_out"] < st2["launches"] - lone, (st, st2)
+    assert base.items() <= got.items()
+    ac.close()
+
+
+@pytest.mark.gpu
 def test_pages_allocator():
     import pech_amd as P
     from pech_amd import _lib

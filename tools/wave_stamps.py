@@ -116,6 +116,52 @@ if cfg == "c3" and (q1 > 0).all():
             prog[:-1] += ov / (hi - lo) * per_wave / 4
     rate = prog[:-1] / 5e-6 / 1e9
     print("HBM read rate by 5 us bin (GB/s):", [int(x) for x in rate])
+# C4: each wave's size class (host replica of the plan kernel's order: chunks of
+# 1,024 buffers, stably sorted by class, smallest first; static shares of the
+# row space as wave_share's proportional split) -> busy / end by class
+if cfg == "c4":
+    G = 256
+    rows = (sizes // 128).astype(np.int64)  # (aligned: whole lines)
+    order = []
+    for c0 in range(0, len(rows), 1024):
+        ch = np.arange(c0, min(c0 + 1024, len(rows)))
+        order.append(ch[np.argsort(np.minimum(rows[ch], 2048), kind="stable")])  # class cap PECH_LARGE_ROWS
+    order = np.concatenate(order)
+    rcum = np.concatenate([[0], np.cumsum(rows[order])])
+    Rtot = int(rcum[-1])
+    cls_of = {32: "4k", 512: "64k", 8192: "1m", 32768: "4m"}
+    lab = []
+    for w in wid:
+        b, wv = divmod(int(w), wpg)
+        wg0 = b * Rtot // G
+        wgr = (b + 1) * Rtot // G - wg0
+        r0, r1 = wg0 + wgr * wv // wpg, wg0 + wgr * (wv + 1) // wpg
+        i0 = np.searchsorted(rcum, r0, side="right") - 1
+        i1 = np.searchsorted(rcum, r1 - 1, side="right") - 1
+        got = {}
+        for i in range(i0, i1 + 1):
+            ov = min(r1, rcum[i + 1]) - max(r0, rcum[i])
+            k = cls_of.get(int(rows[order[i]]), "?")
+            got[k] = got.get(k, 0) + ov
+        lab.append(max(got, key=got.get))
+    lab = np.asarray(lab)
+    for k in ("4k", "64k", "1m", "4m"):
+        m = lab == k
+        if m.any():
+            print(f"class {k}: waves {int(m.sum())} busy p50 {pct(busy[m], 50):.1f} p90 {pct(busy[m], 90):.1f} "
+                  f"end p50 {pct(e[m], 50) / 100:.1f} p90 {pct(e[m], 90) / 100:.1f} max {e[m].max() / 100:.1f} us")
+    # per workgroup: its last wave's end against its share of small-class rows
+    wgl = {}
+    for w, t, k in zip(wid, e, lab):
+        d = wgl.setdefault(int(w) // wpg, [0, 0])
+        d[0] = max(d[0], int(t))
+        d[1] += k in ("4k", "64k")
+    arr = np.array(list(wgl.values()))
+    for lo, hi in ((0, 0), (1, 8), (9, 15), (16, 16)):
+        m = (arr[:, 1] >= lo) & (arr[:, 1] <= hi)
+        if m.any():
+            print(f"workgroups with {lo}-{hi} small-class waves: {int(m.sum())}, last end p50 {pct(arr[m, 0], 50) / 100:.1f} "
+                  f"max {arr[m, 0].max() / 100:.1f} us")
 out_dir = os.path.join(REPO, "gpurun_out")
 os.makedirs(out_dir, exist_ok=True)
 np.savez(os.path.join(out_dir, f"stamps_{cfg}.npz"), start=s, end=e, entry=ent, tag=tag, wid=wid)
