@@ -1124,7 +1124,8 @@ __device__ __forceinline__ uint32_t share_head(uint32_t a, uint32_t b)
 // busy p50 85 / 108 / 134 / 149 us by age slot, profiles/r05/stamps_c4.txt),
 // and the CU's last quarter ran on a quarter of its waves.  Raising the
 // waves that are behind keeps a CU's waves within about a quarter of a share
-// of each other.  (Pooled and interleaved walks balance otherwise.)
+// of each other (profiles/r05/ab_prio.txt).  Pooled walks use the same
+// levels over the rows a wave still holds once its pool is dry (main_body).
 #ifndef PECH_PRIO_MIN_SHARE
 #define PECH_PRIO_MIN_SHARE 1024u
 #endif
@@ -1819,7 +1820,16 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			flat_publish(flag, 0u, n, lane, out, hout);
 		if (!live)
 			return; // whole workgroup idle (small batch)
+		// Flat launches fill late at every size: with the wave-major shares of
+		// small launches only ~4 waves per CU stream, and the early fill's
+		// barrier after all 16 prologues cost them more than the fill behind
+		// their primes (32 MiB 14.1 -> 13.8 us, 4 MiB 10.7 -> 10.4 us,
+		// profiles/r05/ab_curve_v30.txt; PECH_FLAT_EARLY_FILL: the old rule)
+#ifdef PECH_FLAT_EARLY_FILL
 		early_fill = !PECH_IL_CRC && Rtot <= (uint64_t)PECH_EARLY_FILL_ROWS * gridDim.x; // workgroup-uniform
+#else
+		early_fill = false;
+#endif
 		if (early_fill) {
 			fill_tables(false);
 			__syncthreads();
@@ -1961,9 +1971,34 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	const bool prio_on = !COPY && jmax == 0u && !il && rem_all >= PECH_PRIO_MIN_SHARE;
 #endif
 	Prio prio = prio_init(rem_all);
+#ifndef PECH_NO_PRIO_POOL
+	// Pooled walks (uniform batches of buffers of >= PECH_SPLIT_ROWS rows):
+	// once a wave's latest claim finds the pool dry, the waves holding the
+	// most rows go first.  Claims run two items ahead, so the oldest waves
+	// used to finish their last two items first and leave the CU to the
+	// youngest: C3 end p50 131 / 141 / 148 / 154 us by age slot, per-CU end
+	// spread 25 us; with it 11 us, 162.1 -> 160.6 us per launch, serial
+	// +0.9 %, value unchanged (profiles/r05/ab_prio_pool.txt).  (1 GiB of
+	// 4 KiB buffers lost 3-4 % of its sustained rate with it.)
+	const bool prio_pool = !COPY && jmax > 1u && sv.U0 >= PECH_SPLIT_ROWS;
+	if (prio_pool)
+		prio = prio_init(2u * PECH_ITEM_ROWS);
+	// rows this wave has left: unknown (max) while its latest claim still got an item
+	auto pool_left = [&](uint32_t in_step) -> uint32_t {
+		const uint32_t c1 = uni(claim), c2 = uni(claim2);
+		if (1u + (c2 >> 4) < jmax)
+			return 0xFFFFFFFFu;
+		return in_step + (1u + (c1 >> 4) < jmax ? PECH_ITEM_ROWS : 0u);
+	};
+#else
+	constexpr bool prio_pool = false;
+	auto pool_left = [](uint32_t in_step) -> uint32_t { return in_step; };
+#endif
 	while (S.T) {
 		if (prio_on)
 			prio_update(prio, S.rem + 8u * S.T);
+		if (prio_pool)
+			prio_update(prio, pool_left(S.rem + 8u * S.T));
 		uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 		// row 0's bytes before the buffer are zeros (free: leading zeros):
 		// zoff -> the whole piece, zh -> its first zh bytes; on 64-bit halves
@@ -1982,6 +2017,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			const uint64_t base = S.ad + (uint64_t)blk * U * rsb;
 			if (prio_on && blk)
 				prio_update(prio, S.rem + 8u * (S.T - blk * U));
+			if (prio_pool && blk)
+				prio_update(prio, pool_left(S.rem + 8u * (S.T - blk * U)));
 #if defined(PECH_STAMPS) && !defined(PECH_STAMP_FIN)
 			if (nstep == 0 && (blk == nblk / 4u || blk == nblk / 2u || blk == 3u * nblk / 4u))
 				tq[blk == nblk / 4u ? 0 : (blk == nblk / 2u ? 1 : 2)] = __builtin_amdgcn_s_memrealtime();
@@ -2702,6 +2739,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.30 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.30 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }
