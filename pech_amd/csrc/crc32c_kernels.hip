@@ -1797,8 +1797,13 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// from the waves still in their prologue and the tail grew
 	// (profiles/r04/ab_early_fill.txt).  The copy kernel's table depends on
 	// the scan (interleaved mode): late fill.
-	// (Flat batches know the launch's rows exactly before they decide: the
-	// scan of their descriptors needs no further load.)
+	// The estimate's limit: it is chunk 0's rows times the chunk
+	// count, so a skewed batch -- small buffers in its first 1,024, large ones
+	// after -- can take the early fill at a size where the late one is faster
+	// (a tail ~1 us longer, never a wrong result).  The exact total would
+	// need a load after the scan, i.e. a round trip before the fill on every
+	// planned launch; the messenger's and the benchmarks' batches are not
+	// skewed that way.  (Flat batches fill late at every size.)
 	Start sv;
 	bool early_fill, live;
 	if constexpr (FLAT) {

@@ -15,7 +15,7 @@ import csv
 import json
 import sys
 
-KERNELS = ("pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct", "pech_crc32c_direct_copy")
+KERNELS = ("pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct", "pech_crc32c_direct_copy", "pech_crc32c_flat")
 
 
 def per_launch_kib(path, counter):
