@@ -1991,9 +1991,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// rows this wave has left: unknown (max) while its latest claim still got an item
 	auto pool_left = [&](uint32_t in_step) -> uint32_t {
 		const uint32_t c1 = uni(claim), c2 = uni(claim2);
-		if (1u + (c2 >> 4) < jmax)
+		if (1u + c2 / PECH_MAIN_WAVES < jmax)
 			return 0xFFFFFFFFu;
-		return in_step + (1u + (c1 >> 4) < jmax ? PECH_ITEM_ROWS : 0u);
+		return in_step + (1u + c1 / PECH_MAIN_WAVES < jmax ? PECH_ITEM_ROWS : 0u);
 	};
 #else
 	constexpr bool prio_pool = false;
@@ -2093,7 +2093,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			// item done: the next one from the pool (wave-uniform branch,
 			// scalar work and an LDS atomic; the ring is untouched)
 			for (;;) {
-				const uint32_t c = uni(claim), j = 1u + (c >> 4), sh = c & 15u;
+				const uint32_t c = uni(claim), j = 1u + c / PECH_MAIN_WAVES, sh = c % PECH_MAIN_WAVES;
 				if (j >= jmax)
 					break; // pool empty
 				const uint32_t a = (uint32_t)(wg0 + (uint64_t)wg_rows * sh / PECH_MAIN_WAVES);
@@ -2127,7 +2127,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				// N ends a pooled item: the next item is the pending claim's
 				// (a guess: an item past its share's end moves on to the next
 				// claim, and the plan then misses and loads)
-				const uint32_t c = uni(claim), j = 1u + (c >> 4), sh = c & 15u;
+				const uint32_t c = uni(claim), j = 1u + c / PECH_MAIN_WAVES, sh = c % PECH_MAIN_WAVES;
 				const uint32_t a = (uint32_t)(wg0 + (uint64_t)wg_rows * sh / PECH_MAIN_WAVES);
 				const uint32_t b = (uint32_t)(wg0 + (uint64_t)wg_rows * (sh + 1u) / PECH_MAIN_WAVES);
 				const uint32_t st = share_head(a, b) + (j - 1u) * PECH_ITEM_ROWS;
