@@ -60,6 +60,9 @@ CONFIGS = {
     "c4-4m": ([4 << 20] * 64, 4, "c4 class 4 MiB: 64 x 4 MiB per launch"),
     # C2's 4 KiB buffers in a 1 GiB launch (the size class of C4 that costs most, at C3's launch size)
     "c2-1g": ([4096] * 262144, 2, "c2-1g: 262,144 x 4 KiB (1 GiB) per launch, 2 rotating batches"),
+    # small launches (the launch curve's points as configs, for PMC passes): 4 MiB and 32 MiB of 4 MiB buffers
+    "l4m": ([4 << 20], 8, "l4m: one 4 MiB buffer per launch, 8 rotating batches"),
+    "l32m": ([4 << 20] * 8, 8, "l32m: 8 x 4 MiB per launch, 8 rotating batches"),
     # unaligned payloads (messenger lengths are arbitrary): every buffer has a head and/or a tail
     "c2-odd": ([4100] * 65536, 4, "c2-odd: 65,536 x 4,100 B back to back (unaligned heads and tails), 4 rotating batches"),
 }
