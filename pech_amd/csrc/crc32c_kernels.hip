@@ -42,6 +42,13 @@
 #ifndef PECH_U_COPY
 #define PECH_U_COPY 12 // rows per block, fused-copy variant (block discipline, 128 VGPRs)
 #endif
+#ifndef PECH_SPLIT_MIN
+#define PECH_SPLIT_MIN 8u // rows of a large buffer a step splits over the 8 groups (plan_step; >= 8: a row each)
+#endif
+static_assert(PECH_SPLIT_MIN >= 8u, "every slice of a split step needs a row");
+#ifndef PECH_LIVE_WAVES
+#define PECH_LIVE_WAVES 4u // small launches: the live waves per CU wave_share aims at
+#endif
 #ifndef PECH_MAIN_WAVES
 #define PECH_MAIN_WAVES 16 // waves per main-kernel workgroup (one workgroup per CU)
 #endif
@@ -722,10 +729,16 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 		const uint32_t meta0 = uni(cd.meta);
 		const uint32_t avail0 = rows0 - lr;
 		// A large buffer (or what is left of it) goes to 8 slices when at least
-		// 64 of its rows are to be walked: a remainder below PECH_SPLIT_ROWS
-		// walked by group 0 alone left 7 groups idle (up to 255 rows; 19 % of
-		// the row slots of a C4-like mix in tests/kernel_model.py).
-		if (rows0 >= PECH_SPLIT_ROWS && min(avail0, rem) >= 64u) {
+		// PECH_SPLIT_MIN (8) of its rows are to be walked, so every slice has a
+		// row.  A remainder walked by group 0 alone left 7 groups idle: below
+		// PECH_SPLIT_ROWS, 19 % of the row slots of a C4-like mix
+		// (tests/kernel_model.py); below 64 rows (v0.17-v0.30), every share
+		// that ends a few rows into a buffer or starts a few rows before its
+		// end -- launches whose rows per wave do not divide the buffers: 8 x
+		// 4,100,000 B took 21.0 us against 14.2 us for 8 x 4 MiB
+		// (profiles/r05/launch_sizes.txt).  The slices' folds and shifts run
+		// side by side, so short slices cost no more than one group's run.
+		if (rows0 >= PECH_SPLIT_ROWS && min(avail0, rem) >= PECH_SPLIT_MIN) {
 			// one large buffer (portion): 8 contiguous slices, one per group
 			const uint32_t P = min(avail0, rem);
 			const uint32_t q = P >> 3, rm = P & 7u;
@@ -1185,7 +1198,7 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 	// spend less of it in per-wave work (32 MiB: 15.2 -> 13.4 us,
 	// profiles/r05/ab_wave_major.txt); from W 4 rpw_min rows on, every wave
 	// of every CU streams its proportional share.
-	const uint32_t G4 = 4u * gridDim.x;
+	const uint32_t G4 = PECH_LIVE_WAVES * gridDim.x;
 	const uint32_t rpw_a = min(max((uint32_t)(((uint64_t)Rtot + G4 - 1u) / G4), rpw_min), 4u * rpw_min);
 	const bool prop = (uint64_t)Rtot >= (uint64_t)W * rpw_a;
 	const uint32_t rpw = prop ? 0u : rpw_a;
@@ -2744,6 +2757,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.30 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.31 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -28,6 +28,7 @@ def _consts():
     out["PECH_U"] = int(re.search(r"#define PECH_U (\d+)", ksrc).group(1))
     out["PECH_U_COPY"] = int(re.search(r"#define PECH_U_COPY (\d+)", ksrc).group(1))
     out["PECH_MAIN_WAVES"] = int(re.search(r"#define PECH_MAIN_WAVES (\d+)", ksrc).group(1))
+    out["PECH_SPLIT_MIN"] = int(re.search(r"#define PECH_SPLIT_MIN (\d+)u", ksrc).group(1))
     out["PECH_SLOT_W"] = [1, 1, 1, 1]  # the kernel splits a workgroup's rows equally over its waves
     return out
 
@@ -36,6 +37,7 @@ C = _consts()
 ROW = C["PECH_ROW_BYTES"]
 CHUNK = C["PECH_CHUNK"]
 SPLIT = C["PECH_SPLIT_ROWS"]
+SPLIT_MIN = C["PECH_SPLIT_MIN"]
 LARGE = C["PECH_LARGE_ROWS"]
 WAVES_PER_WG = C["PECH_MAIN_WAVES"]
 ITEM = C["PECH_ITEM_ROWS"]
@@ -389,9 +391,9 @@ def walk(cores, nzs, pos, lr, rem, U, events, grid=False):
             avail0 = rows0 - lr
             assert avail0 > 0
             # a large buffer (or what is left of it) goes to 8 slices when at
-            # least 64 of its rows are to be walked: a remainder walked by
-            # group 0 alone left 7 groups idle (up to 255 rows)
-            if rows0 >= SPLIT and min(avail0, rem) >= 64:
+            # least SPLIT_MIN (8) of its rows are to be walked: a remainder
+            # walked by group 0 alone left 7 groups idle
+            if rows0 >= SPLIT and min(avail0, rem) >= SPLIT_MIN:
                 P = min(avail0, rem)
                 q, rm = P >> 3, P & 7
                 T = q + (1 if rm else 0)
