@@ -164,4 +164,5 @@ if cfg == "c4":
                   f"max {arr[m, 0].max() / 100:.1f} us")
 out_dir = os.path.join(REPO, "gpurun_out")
 os.makedirs(out_dir, exist_ok=True)
-np.savez(os.path.join(out_dir, f"stamps_{cfg}.npz"), start=s, end=e, entry=ent, tag=tag, wid=wid)
+np.savez(os.path.join(out_dir, f"stamps_{cfg}.npz"), start=s, end=e, entry=ent, tag=tag, wid=wid, q1=q1, q2=q2, q3=q3,
+         tplan=tplan, tfill=tfill, tfind=tfind)
