@@ -1086,7 +1086,7 @@ __device__ __forceinline__ void finish_run(uint32_t *lds, uint32_t g8, uint32_t 
 				atomicXor(out + o0, v);
 		}
 	} else if (active && g8 == 0) {
-#ifdef PECH_AB_NOATOMIC // diagnostic build only: run results of non-split steps dropped (wrong CRCs)
+#ifdef PECH_AB_NOATOMIC // diagnostic build only: run results of non-split steps dropped (wrong CRCs; the deferral flush too)
 		if (v == 0x9E3779B9u)
 #endif
 		atomicXor(out + orig, v);
@@ -2239,6 +2239,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			}
 #endif
 			if (flush)
+#ifdef PECH_AB_NOATOMIC // diagnostic build only: the flush dropped too (wrong CRCs)
+				if (k == 0x9E3779B9u)
+#endif
 				atomicXor(out + k, lds[L_DEFER / 4u + PECH_DEFER_SLOTS + lane]);
 			if (FLAT && hout)
 				flat_publish(flag, sv.nlive, n, lane, out, hout);
