@@ -1219,7 +1219,21 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 	// with interleaved rows: they walk the workgroup's range together.)
 	st.nlive = prop ? gridDim.x : (uint32_t)min((uint64_t)gridDim.x, ((uint64_t)Rtot + rpw - 1u) / rpw);
 	if (!prop && !il) {
-		const uint64_t k = (uint64_t)wave * gridDim.x + blockIdx.x;
+#ifdef PECH_DEAL_FULL_GRID // A/B: the shares dealt over every workgroup (v0.29c-v0.31)
+		const uint32_t Gd = gridDim.x;
+#else
+		// ... over just enough workgroups for PECH_LIVE_WAVES live waves each:
+		// below 4 G rpw_min rows (8 MiB on 256 CUs) fewer workgroups carry the
+		// launch, and each buffer's out[] word gets fewer cross-workgroup XORs
+		// (a 4 MiB launch: 128 instead of 256 onto one word; those atomics cost
+		// small launches 1.5-2 us, profiles/r05/ab_share_dealing.txt)
+		const uint32_t nsh = (uint32_t)(((uint64_t)Rtot + rpw - 1u) / rpw);
+		const uint32_t Gd = min(gridDim.x, (nsh + PECH_LIVE_WAVES - 1u) / PECH_LIVE_WAVES);
+		st.nlive = min(st.nlive, Gd);
+		if (blockIdx.x >= Gd)
+			return false; // whole workgroup idle
+#endif
+		const uint64_t k = (uint64_t)wave * Gd + blockIdx.x;
 		if ((uint64_t)blockIdx.x * rpw >= Rtot)
 			return false; // whole workgroup idle: its wave 0 has the lowest share
 		const uint64_t a = k * rpw;
@@ -2760,6 +2774,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.31 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.32 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

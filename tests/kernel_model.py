@@ -222,7 +222,7 @@ def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None, il=False, by_
     contiguous pieces inside (by age-rank weight in the model's A/B
     variants).  Small ones: shares of rpw rows -- rpw from rpw_min up to 4
     rpw_min, aiming at four live waves per CU -- dealt wave-major (share k =
-    wave * ncu + workgroup), except in the fused copy's interleaved mode,
+    wave * Gd + workgroup, over Gd = min(ncu, ceil(shares / 4)) workgroups), except in the fused copy's interleaved mode,
     which walks each workgroup's contiguous range.  by_wg: a list per live
     workgroup, and whether the launch is proportional."""
     rpw_min = rpw_min or C["PECH_RPW_MIN"]
@@ -236,9 +236,11 @@ def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None, il=False, by_
     out = []
     for b in range(ncu):
         if not prop and not il:
-            if b * rpw >= Rtot:
+            nsh = (Rtot + rpw - 1) // rpw
+            Gd = min(ncu, (nsh + 3) // 4)  # just enough workgroups for four live waves each
+            if b >= Gd or b * rpw >= Rtot:
                 continue
-            out.append([(min((w * ncu + b) * rpw, Rtot), min((w * ncu + b) * rpw + rpw, Rtot)) for w in range(waves)])
+            out.append([(min((w * Gd + b) * rpw, Rtot), min((w * Gd + b) * rpw + rpw, Rtot)) for w in range(waves)])
             continue
         wg0 = b * Rtot // ncu if prop else b * waves * rpw
         if wg0 >= Rtot:
