@@ -46,6 +46,9 @@
 #define PECH_SPLIT_MIN 8u // rows of a large buffer a step splits over the 8 groups (plan_step; >= 8: a row each)
 #endif
 static_assert(PECH_SPLIT_MIN >= 8u, "every slice of a split step needs a row");
+#ifndef PECH_DEAL_BLOCKS
+#define PECH_DEAL_BLOCKS 32u // small launches: a workgroup's live shares lie this many apart (wave_share)
+#endif
 #ifndef PECH_LIVE_WAVES
 #define PECH_LIVE_WAVES 4u // small launches: the live waves per CU wave_share aims at
 #endif
@@ -1233,9 +1236,28 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 		if (blockIdx.x >= Gd)
 			return false; // whole workgroup idle
 #endif
+#if PECH_DEAL_BLOCKS
+		// ... in blocks of 4 S shares, S = PECH_DEAL_BLOCKS: a workgroup's live
+		// shares lie S apart inside one block (one buffer as a rule, so the
+		// workgroup's deferral table sends one atomic per buffer; not
+		// neighbours: two waves of a CU on neighbouring ranges of a buffer
+		// cost more than the atomics they save).  64 x 500 KiB 17.0 -> 14.0 us,
+		// 4 MiB of 64 KiB buffers 10.1-10.5 -> 8.3-8.7 us
+		// (profiles/r05/ab_deal_blocks.txt).  (-DPECH_DEAL_BLOCKS=0: strided.)
+		constexpr uint32_t S = PECH_DEAL_BLOCKS;
+		const uint64_t k = Gd % S == 0u && wave < PECH_LIVE_WAVES
+					   ? (uint64_t)(blockIdx.x / S) * (PECH_LIVE_WAVES * S) + blockIdx.x % S + S * wave
+					   : (uint64_t)wave * Gd + blockIdx.x;
+		if (Gd % S == 0u) // live: the workgroups whose first share exists (every full block's S, the last one's first)
+			st.nlive = nsh / (PECH_LIVE_WAVES * S) * S + min(nsh % (PECH_LIVE_WAVES * S), S);
+		if (Gd % S == 0u ? (uint64_t)(blockIdx.x / S) * (PECH_LIVE_WAVES * S) + blockIdx.x % S >= nsh
+				 : (uint64_t)blockIdx.x * rpw >= Rtot)
+			return false; // whole workgroup idle: its wave 0 has the lowest share
+#else
 		const uint64_t k = (uint64_t)wave * Gd + blockIdx.x;
 		if ((uint64_t)blockIdx.x * rpw >= Rtot)
 			return false; // whole workgroup idle: its wave 0 has the lowest share
+#endif
 		const uint64_t a = k * rpw;
 		st.r0 = (uint32_t)min(a, (uint64_t)Rtot);
 		st.r1 = (uint32_t)min(a + rpw, (uint64_t)Rtot);
@@ -2774,6 +2796,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.32 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.32 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -29,6 +29,7 @@ def _consts():
     out["PECH_U_COPY"] = int(re.search(r"#define PECH_U_COPY (\d+)", ksrc).group(1))
     out["PECH_MAIN_WAVES"] = int(re.search(r"#define PECH_MAIN_WAVES (\d+)", ksrc).group(1))
     out["PECH_SPLIT_MIN"] = int(re.search(r"#define PECH_SPLIT_MIN (\d+)u", ksrc).group(1))
+    out["PECH_DEAL_BLOCKS"] = int(re.search(r"#define PECH_DEAL_BLOCKS (\d+)u", ksrc).group(1))
     out["PECH_SLOT_W"] = [1, 1, 1, 1]  # the kernel splits a workgroup's rows equally over its waves
     return out
 
@@ -38,6 +39,7 @@ ROW = C["PECH_ROW_BYTES"]
 CHUNK = C["PECH_CHUNK"]
 SPLIT = C["PECH_SPLIT_ROWS"]
 SPLIT_MIN = C["PECH_SPLIT_MIN"]
+DEAL_BLOCKS = C["PECH_DEAL_BLOCKS"]
 LARGE = C["PECH_LARGE_ROWS"]
 WAVES_PER_WG = C["PECH_MAIN_WAVES"]
 ITEM = C["PECH_ITEM_ROWS"]
@@ -221,8 +223,10 @@ def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None, il=False, by_
     Large launches (Rtot >= W * rpw): proportional workgroup ranges, equal
     contiguous pieces inside (by age-rank weight in the model's A/B
     variants).  Small ones: shares of rpw rows -- rpw from rpw_min up to 4
-    rpw_min, aiming at four live waves per CU -- dealt wave-major (share k =
-    wave * Gd + workgroup, over Gd = min(ncu, ceil(shares / 4)) workgroups), except in the fused copy's interleaved mode,
+    rpw_min, aiming at four live waves per CU -- dealt over Gd = min(ncu,
+    ceil(shares / 4)) workgroups, in blocks of 4 S shares (a workgroup's live
+    shares S apart) when Gd is a multiple of S, else wave-major (k = wave *
+    Gd + workgroup), except in the fused copy's interleaved mode,
     which walks each workgroup's contiguous range.  by_wg: a list per live
     workgroup, and whether the launch is proportional."""
     rpw_min = rpw_min or C["PECH_RPW_MIN"]
@@ -238,9 +242,13 @@ def wave_ranges(Rtot, ncu, rpw_min=None, weights=None, waves=None, il=False, by_
         if not prop and not il:
             nsh = (Rtot + rpw - 1) // rpw
             Gd = min(ncu, (nsh + 3) // 4)  # just enough workgroups for four live waves each
-            if b >= Gd or b * rpw >= Rtot:
+            S = DEAL_BLOCKS
+            blocks = S and Gd % S == 0
+            first = (b // S) * 4 * S + b % S if blocks else b
+            if b >= Gd or first * rpw >= Rtot:
                 continue
-            out.append([(min((w * Gd + b) * rpw, Rtot), min((w * Gd + b) * rpw + rpw, Rtot)) for w in range(waves)])
+            ks = [(b // S) * 4 * S + b % S + S * w if blocks and w < 4 else w * Gd + b for w in range(waves)]
+            out.append([(min(k * rpw, Rtot), min(k * rpw + rpw, Rtot)) for k in ks])
             continue
         wg0 = b * Rtot // ncu if prop else b * waves * rpw
         if wg0 >= Rtot:
