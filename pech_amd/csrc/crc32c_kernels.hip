@@ -1248,8 +1248,11 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 		const uint64_t k = Gd % S == 0u && wave < PECH_LIVE_WAVES
 					   ? (uint64_t)(blockIdx.x / S) * (PECH_LIVE_WAVES * S) + blockIdx.x % S + S * wave
 					   : (uint64_t)wave * Gd + blockIdx.x;
-		if (Gd % S == 0u) // live: the workgroups whose first share exists (every full block's S, the last one's first)
-			st.nlive = nsh / (PECH_LIVE_WAVES * S) * S + min(nsh % (PECH_LIVE_WAVES * S), S);
+		// live: the workgroups whose first share exists (every full block's S,
+		// the last one's first ones; all Gd once there are more shares than
+		// the blocks hold -- the waves past PECH_LIVE_WAVES take those)
+		if (Gd % S == 0u)
+			st.nlive = min(Gd, nsh / (PECH_LIVE_WAVES * S) * S + min(nsh % (PECH_LIVE_WAVES * S), S));
 		if (Gd % S == 0u ? (uint64_t)(blockIdx.x / S) * (PECH_LIVE_WAVES * S) + blockIdx.x % S >= nsh
 				 : (uint64_t)blockIdx.x * rpw >= Rtot)
 			return false; // whole workgroup idle: its wave 0 has the lowest share

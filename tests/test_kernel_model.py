@@ -197,3 +197,34 @@ def test_final_shift_packing_at_maximum_length():
                 assert mp < 1 << 32
                 assert KM.decode_m(mp, oz) == ra * KM.ROW + tail - 16 * zt, (addr, ln, ra)
     assert KM.core_rows(127, (1 << 32) - 1) == (1 << 25) + 1  # the case exists
+
+
+def test_small_launch_live_workgroups_count():
+    """The flat kernel's in-launch publication (flat_publish, the async
+    layer's host array) waits for st.nlive workgroups: the count must equal
+    the workgroups wave_share keeps live for every launch size, and their
+    shares must cover each share exactly once -- the blocked dealing's first
+    count missed that past 4 G shares the waves beyond the fourth take the
+    rest (a 32 MiB + 256-row launch counted 257 live workgroups of 256, so no
+    workgroup published and the host read stale results)."""
+    G, LW, S = 256, 4, KM.DEAL_BLOCKS
+    W = G * KM.WAVES_PER_WG
+    for Rtot in list(range(1, 70000, 7)) + list(range(70000, 1100000, 997)):
+        rpw = min(max((Rtot + LW * G - 1) // (LW * G), 64), 256)
+        if Rtot >= W * rpw:
+            continue
+        nsh = (Rtot + rpw - 1) // rpw
+        Gd = min(G, (nsh + LW - 1) // LW)
+        blocks = S and Gd % S == 0
+        nl = min(Gd, nsh // (LW * S) * S + min(nsh % (LW * S), S)) if blocks else min(G, nsh, Gd)
+        live, cov = 0, [0] * nsh
+        for b in range(Gd):
+            first = (b // S) * LW * S + b % S if blocks else b
+            if (first >= nsh) if blocks else (b * rpw >= Rtot):
+                continue
+            live += 1
+            for w in range(KM.WAVES_PER_WG):
+                k = (b // S) * LW * S + b % S + S * w if blocks and w < LW else w * Gd + b
+                if k < nsh:
+                    cov[k] += 1
+        assert live == nl and all(c == 1 for c in cov), (Rtot, rpw, nsh, Gd, nl, live)
