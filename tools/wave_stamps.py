@@ -15,6 +15,9 @@ if cfg == "c3":
     sizes = np.full(256, 4 << 20, dtype=np.int64)
 elif cfg.endswith("x4m"):  # launch-size series: <n> x 4 MiB
     sizes = np.full(int(cfg[:-3]), 4 << 20, dtype=np.int64)
+elif "x" in cfg and cfg.split("x")[0].isdigit():  # <n>x<bytes>[k|m] (tools/launch_sizes.py shapes)
+    n, sz = cfg.split("x")
+    sizes = np.full(int(n), int(sz.rstrip("km")) * {"k": 1 << 10, "m": 1 << 20}.get(sz[-1], 1), dtype=np.int64)
 elif cfg == "c4":  # bench.py's c4_sizes: equal bytes per class, shuffled with seed 42
     sizes = [4096] * 65536 + [65536] * 4096 + [1 << 20] * 256 + [4 << 20] * 64
     np.random.default_rng(42).shuffle(sizes)
