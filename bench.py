@@ -647,8 +647,8 @@ def msgr_latency(args):
 
 
 def launch_curve(shard, P, torch):
-    """Per-launch cost of the planned path (plan + main kernels) against
-    launch size, for 4 MiB and 64 KiB buffers: 4 / 32 (the async layer's
+    """Per-launch cost of the device batch path (the flat kernel for up to
+    256 buffers, plan + main kernels beyond) against launch size, for 4 MiB and 64 KiB buffers: 4 / 32 (the async layer's
     slot) / 128 / 256 / 1024 MiB per launch, carved from the shard's resident
     batches and cycled over distinct regions of them (2 GiB in all, so the
     256 MB Infinity Cache cannot serve a launch).  main_us: HIP events around
@@ -695,7 +695,8 @@ def launch_curve(shard, P, torch):
                              "step_us": round(step_us, 2), "launches": k}
         res["4MiB" if bsz == 4 << 20 else "64KiB"] = row
     return {"unit": "us per launch; frac = launch bytes / main_us / 8 TB/s", "by_buffer_size_then_MiB": res,
-            "path": "crc32c_dev_batch_ws_async (plan + main), one stream"}
+            "path": "crc32c_dev_batch_ws_async, one stream: the flat kernel for up to 256 buffers (--flat-max), "
+                    "plan + main kernels beyond"}
 
 
 def sustain(shards, nstreams, seconds, sync_all, dist, backend, dev, torch):
