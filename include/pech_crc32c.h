@@ -169,6 +169,11 @@ struct crc32c_stats {
 	uint64_t cpu_calls, cpu_bytes;  /* computed on the host (incl. fallbacks) */
 	uint64_t gpu_calls, gpu_bytes;  /* computed by the gfx950 kernels          */
 	uint64_t gpu_fallbacks;         /* GPU path failed, recomputed on the host */
+	uint64_t gpu_faults;            /* flat launches whose results the kernel itself
+	                                   voided (a wave's wait for out[]'s
+	                                   initialisation timed out): the synchronous
+	                                   and async paths discard them; a device
+	                                   entry point's caller must too */
 };
 int crc32c_get_stats(struct crc32c_stats *st);
 

@@ -148,6 +148,11 @@ struct crc32c_async_stats {
 	unsigned int queued;    /* CRC32C_ASYNC_DMA: filled slots waiting to launch */
 	uint64_t host_out;      /* launches whose kernel stored the results in host memory itself */
 	uint64_t polled;        /* launches whose completion the context's thread polled */
+	uint64_t faults;        /* flat launches whose results the kernel voided: their
+	                           payloads failed with -EIO (no CRC delivered)       */
+	uint64_t pub_missing;   /* flat launches whose in-kernel results publication
+	                           was missing: the results were copied from the GPU
+	                           instead (never a previous batch's)                 */
 };
 int crc32c_async_get_stats(const struct crc32c_async *a, struct crc32c_async_stats *st);
 

@@ -90,8 +90,17 @@ struct crc32c_async *crc32c_msgr_conn_async(const struct crc32c_msgr_conn *c);
  * in the environment) are checksummed at once on the host instead of the
  * GPU: below the crossover the host routine costs less CPU time than the
  * GPU round trip.  Process-wide; returns the previous
- * value.  0 sends every checked payload to the GPU. */
+ * value.  0 sends every checked payload to the GPU (lone ones too, below). */
 unsigned int crc32c_msgr_set_host_max(unsigned int bytes);
+
+/* Payloads of at most `bytes` (default 256 KiB, or PECH_CRC32C_MSGR_LONE_MAX
+ * in the environment) that arrive while the connection's async context has
+ * nothing outstanding (crc32c_async_pending() == 0: queue depth 1) are
+ * checksummed on the host as well: a lone payload cannot share a launch, and
+ * up to this size the host routine costs the thread less CPU than the GPU
+ * round trip, at a fraction of its latency.  Process-wide;
+ * returns the previous value.  0 turns the rule off. */
+unsigned int crc32c_msgr_set_lone_max(unsigned int bytes);
 
 /* RECEIVE, at the footer (read_partial_message :2816): queue msg, whose data
  * section is data[0, len).  check != 0 (do_datacrc and the footer has no
@@ -152,6 +161,8 @@ struct crc32c_msgr_stats {
 	uint64_t rx_submitted, rx_unchecked, rx_verified, rx_bad, rx_released;
 	uint64_t tx_submitted, tx_known, tx_held, tx_released; /* held: footers that had to wait */
 	uint64_t rx_host, tx_host; /* checksummed on the host: small payloads, refused submissions */
+	uint64_t rx_lone, tx_lone; /* of them: payloads up to crc32c_msgr_set_lone_max() routed to the
+	                              host because their context had nothing outstanding */
 };
 void crc32c_msgr_get_stats(struct crc32c_msgr_stats *st);
 

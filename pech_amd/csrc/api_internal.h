@@ -17,8 +17,12 @@
 // host array of n words, or NULL): returns 1 when the results are stored
 // there by the kernel itself, 0 when they are in d_out (the caller copies),
 // a negative errno on failure.
+// hstat (the device view of a coherent pinned host word, or NULL): a flat
+// launch's status word (layout.h PECH_FLAT_PUB / PECH_FLAT_ERR); *flat_tag:
+// that launch's tag, 0 when the batch did not run as one flat launch.
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-				     size_t ws_bytes, hipStream_t stream, bool small = false, uint32_t *hout = nullptr);
+				     size_t ws_bytes, hipStream_t stream, bool small = false, uint32_t *hout = nullptr,
+				     uint64_t *hstat = nullptr, uint64_t *flat_tag = nullptr);
 // The GPUs a multi-device caller spreads over: PECH_DEVICES="0,0,..." (a
 // repeated id puts several shards or contexts on one GPU: how one-GPU boxes
 // rehearse eight) or every visible device.  Count, or a negative errno.
@@ -57,7 +61,9 @@ enum pech_fault_site {
 	PECH_FAULT_ASYNC_LAUNCH = 1, // async: a slot's kernel launch fails
 	PECH_FAULT_ASYNC_DMA = 2,    // async: a payload's H2D DMA fails
 	PECH_FAULT_ASYNC_STREAM = 3, // async: a launched batch's stream fails (no host function, query error)
-	PECH_FAULT_SITES = 4
+	PECH_FAULT_FLAT_TIMEOUT = 4, // a flat launch's waves time out waiting for out[] (PECH_FLAT_T_TIMEOUT)
+	PECH_FAULT_FLAT_NOPUB = 5,   // a flat launch skips its async slot's publication (PECH_FLAT_T_NOPUB)
+	PECH_FAULT_SITES = 6
 };
 PECH_HIDDEN bool pech_fault(int site);
 

@@ -43,7 +43,9 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *, uint32_t, const uint
 extern "C" hipError_t pech_launch_small(const void *, uint32_t, uint32_t, const uint32_t *, uint32_t *, uint32_t,
 					hipStream_t);
 extern "C" hipError_t pech_launch_flat(const pech_desc *, uint32_t, const uint32_t *, uint32_t *, uint32_t, uint32_t,
-				       uint64_t *, uint64_t, hipStream_t, hipEvent_t, hipEvent_t, uint32_t *);
+				       uint64_t *, uint64_t, hipStream_t, hipEvent_t, hipEvent_t, uint32_t *, uint64_t *,
+				       uint32_t);
+extern "C" int pech_read_flat_faults(uint64_t *);
 
 // ---------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -148,6 +150,12 @@ struct DevCtx {
 	void *small_src = nullptr;
 	uint32_t *h_small = nullptr, *small_out = nullptr; // result + ticket, coherent pinned memory
 	uint32_t small_ticket = 0;
+	// flat launches' status words (layout.h PECH_FLAT_ERR), coherent pinned
+	// memory: [0] the synchronous host paths' launches (checked after each
+	// wait: flat_check), [1] the device entry points' (the caller reads
+	// crc32c_get_stats().gpu_faults)
+	uint64_t *h_stat = nullptr, *d_stat = nullptr;
+	uint64_t stat_seen = 0; // h_stat[0] at the last flat_check
 	// timing
 	std::vector<TimedLaunch> pending;
 	std::vector<TimedLaunch> free_events;
@@ -195,6 +203,10 @@ static int ctx_get(DevCtx **out)
 			memset(c->h_small, 0, 256); // ticket 0 is never issued
 			HIP_TRY(hipHostGetDevicePointer(&so, c->h_small, 0));
 			c->small_out = (uint32_t *)so;
+			HIP_TRY(hipHostMalloc((void **)&c->h_stat, 64, hipHostMallocCoherent | hipHostMallocMapped));
+			memset(c->h_stat, 0, 64);
+			HIP_TRY(hipHostGetDevicePointer(&so, c->h_stat, 0));
+			c->d_stat = (uint64_t *)so;
 		}
 		for (int i = 0; i < 2; ++i) // two slots' copies may run on two DMA engines at once
 			HIP_TRY(hipStreamCreateWithFlags(&c->s_copy[i], hipStreamNonBlocking));
@@ -308,10 +320,16 @@ static uint64_t flat_tag()
 // d_dsts != NULL: fused CRC + copy (d_dsts[i] receives descriptor i's bytes).
 // hout != NULL (the async layer's slots): a flat launch also stores the
 // results there, a device-visible pinned host array (*published = true).
+// hstat: the device view of the status word a flat launch reports a fault
+// (or its publication) in (layout.h PECH_FLAT_ERR / PECH_FLAT_PUB; NULL:
+// the device entry points' word of the context); *flat_tag: the flat
+// launch's tag (0: no flat launch).
 static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
 			size_t ws_bytes, hipStream_t stream, const uint64_t *d_dsts = nullptr, uint32_t *hout = nullptr,
-			bool *published = nullptr)
+			bool *published = nullptr, uint64_t *hstat = nullptr, uint64_t *flat_tag_out = nullptr)
 {
+	if (flat_tag_out)
+		*flat_tag_out = 0;
 	if (n == 0)
 		return 0;
 	for (unsigned int off = 0; off < n; off += PECH_MAX_BATCH) {
@@ -342,8 +360,15 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 		if (flat)
 		{
 			const bool pub = hout && m == n; // (one launch: a flat batch is)
+			// test library only: the kernel's fault bits (release: always 0)
+			const uint32_t test = (pech_fault(PECH_FAULT_FLAT_TIMEOUT) ? PECH_FLAT_T_TIMEOUT : 0u) |
+					      (pub && pech_fault(PECH_FAULT_FLAT_NOPUB) ? PECH_FLAT_T_NOPUB : 0u);
+			const uint64_t tag = flat_tag();
 			HIP_TRY(pech_launch_flat(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, rpw_min(),
-						 (uint64_t *)ws, flat_tag(), stream, tl.a, tl.b, pub ? hout : nullptr));
+						 (uint64_t *)ws, tag, stream, tl.a, tl.b, pub ? hout : nullptr,
+						 hstat ? hstat : c->d_stat + 1, test));
+			if (flat_tag_out)
+				*flat_tag_out = tag;
 			if (pub && published)
 				*published = true;
 		}
@@ -354,6 +379,21 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			c->pending.push_back(tl);
 	}
 	return 0;
+}
+
+// After a synchronous host path has waited for its launches: a flat launch
+// that reported a fault in the context's status word (layout.h
+// PECH_FLAT_ERR; the word changes only then, and tags never repeat) voids
+// the results of the call -- -EIO, and the drop-in recomputes on the host.
+static int flat_check(DevCtx *c)
+{
+	const uint64_t v = __atomic_load_n(c->h_stat, __ATOMIC_ACQUIRE);
+	if (v == c->stat_seen)
+		return 0;
+	c->stat_seen = v;
+	(void)hipStreamSynchronize(c->s_comp); // nothing of the call still runs when it returns
+	set_err("flat kernel: a wave's wait for out[]'s initialisation timed out; the batch's results are void");
+	return -EIO;
 }
 
 // A device batch on the internal workspace, on the caller's stream: ordered
@@ -413,8 +453,11 @@ static int launch_small(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 // internal entry points for crc32c_async.cpp (hidden: not part of the C-ABI)
 
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
-				     size_t ws_bytes, hipStream_t stream, bool small, uint32_t *hout)
+				     size_t ws_bytes, hipStream_t stream, bool small, uint32_t *hout, uint64_t *hstat,
+				     uint64_t *flat_tag)
 {
+	if (flat_tag)
+		*flat_tag = 0;
 	std::lock_guard<std::mutex> lk(g_mu);
 	DevCtx *c = nullptr;
 	int rc = ctx_get(&c);
@@ -424,7 +467,7 @@ PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, 
 		return hout && n <= PECH_MAX_BATCH ? (launch_small(c, d_descs, hout, n, stream) ?: 1)
 						   : launch_small(c, d_descs, d_out, n, stream);
 	bool pub = false;
-	rc = launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream, nullptr, hout, &pub);
+	rc = launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream, nullptr, hout, &pub, hstat, flat_tag);
 	return rc ? rc : pub ? 1 : 0;
 }
 
@@ -573,7 +616,8 @@ static int enqueue_host_slot(DevCtx *c, int s, const void *const *bufs, const un
 	int rc = ws_host_reserve(c, m);
 	if (rc)
 		return rc;
-	rc = launch_batch(c, c->d_desc[s], c->d_out[s], m, c->d_ws_host, c->ws_host_bytes, c->s_comp);
+	rc = launch_batch(c, c->d_desc[s], c->d_out[s], m, c->d_ws_host, c->ws_host_bytes, c->s_comp, nullptr, nullptr,
+			  nullptr, c->d_stat);
 	if (rc)
 		return rc;
 	HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
@@ -595,6 +639,8 @@ static int host_big(DevCtx *c, const void *buf, size_t len, uint32_t seed, uint3
 		if (rc)
 			return rc;
 		HIP_TRY(hipEventSynchronize(c->ev_done[0]));
+		if ((rc = flat_check(c)))
+			return rc;
 		crc = c->h_out[0][0];
 		p += m;
 		len -= m;
@@ -765,7 +811,8 @@ static int shard_pinned(const void *const *bufs, const unsigned int *lens, const
 				break;
 			}
 			// shards on one device share its stream (ordered), so one workspace serves them
-			if ((rc = launch_batch(c, dd, dout, S.m, c->d_ws_host, c->ws_host_bytes, c->s_comp)))
+			if ((rc = launch_batch(c, dd, dout, S.m, c->d_ws_host, c->ws_host_bytes, c->s_comp, nullptr, nullptr,
+					       nullptr, c->d_stat)))
 				break;
 			if (hipMemcpyAsync(ho, dout, (size_t)S.m * 4u, hipMemcpyDeviceToHost, c->s_comp) != hipSuccess) {
 				set_err("hipMemcpyAsync: %s", hipGetErrorString(hipGetLastError()));
@@ -782,6 +829,8 @@ static int shard_pinned(const void *const *bufs, const unsigned int *lens, const
 				rc = -EIO;
 				break;
 			}
+			if ((rc = flat_check(S.c)))
+				break;
 			memcpy(out + S.i0, S.c->h_out[slot[k]] + off[k], (size_t)S.m * 4u);
 			S.i0 += S.m;
 			more = more || S.i0 < cut[k + 1];
@@ -806,8 +855,10 @@ static int host_batch(DevCtx *c, const void *const *bufs, const unsigned int *le
 		if (!busy[t])
 			return 0;
 		HIP_TRY(hipEventSynchronize(c->ev_done[t]));
-		memcpy(out + slot_i0[t], c->h_out[t], (size_t)slot_m[t] * 4u);
 		busy[t] = false;
+		if (int e = flat_check(c))
+			return e;
+		memcpy(out + slot_i0[t], c->h_out[t], (size_t)slot_m[t] * 4u);
 		return 0;
 	};
 	while (i < n) {
@@ -863,10 +914,13 @@ static int device_batch_sync(DevCtx *c, const void *const *bufs, const unsigned 
 				       c->s_comp));
 		if ((rc = ws_host_reserve(c, m)))
 			return rc;
-		if ((rc = launch_batch(c, c->d_desc[0], c->d_out[0], m, c->d_ws_host, c->ws_host_bytes, c->s_comp)))
+		if ((rc = launch_batch(c, c->d_desc[0], c->d_out[0], m, c->d_ws_host, c->ws_host_bytes, c->s_comp, nullptr,
+				       nullptr, nullptr, c->d_stat)))
 			return rc;
 		HIP_TRY(hipMemcpyAsync(c->h_out[0], c->d_out[0], (size_t)m * 4u, hipMemcpyDeviceToHost, c->s_comp));
 		HIP_TRY(hipStreamSynchronize(c->s_comp));
+		if ((rc = flat_check(c)))
+			return rc;
 		memcpy(out + i0, c->h_out[0], (size_t)m * 4u);
 	}
 	return 0;
@@ -1009,7 +1063,36 @@ int crc32c_get_stats(struct crc32c_stats *st)
 	st->gpu_calls = g_st_gpu_calls.load();
 	st->gpu_bytes = g_st_gpu_bytes.load();
 	st->gpu_fallbacks = g_st_fallbacks.load();
-	return 0;
+	// flat launches that reported a fault, on every initialised device (the
+	// kernels count them: pech_flat_faults)
+	return on_lib_stack([&] {
+		std::lock_guard<std::mutex> lk(g_mu);
+		uint64_t faults = 0;
+		st->gpu_faults = 0;
+		bool any = false;
+		for (int d = 0; d < 64; ++d)
+			any = any || g_ctx[d].dev >= 0;
+		if (!any)
+			return 0; // (no GPU used: no HIP call)
+		int cur = -1;
+		if (hipGetDevice(&cur) != hipSuccess)
+			cur = -1;
+		for (int d = 0; d < 64; ++d) {
+			if (g_ctx[d].dev < 0)
+				continue;
+			uint64_t v = 0;
+			if (hipSetDevice(d) != hipSuccess || pech_read_flat_faults(&v)) {
+				set_err("crc32c_get_stats: reading device %d's fault count failed", d);
+				(void)hipGetLastError();
+				continue;
+			}
+			faults += v;
+		}
+		if (cur >= 0)
+			(void)hipSetDevice(cur);
+		st->gpu_faults = faults;
+		return 0;
+	});
 }
 
 int crc32c_batch(const void *const *bufs, const unsigned int *lens, const uint32_t *seeds, uint32_t *out,

@@ -286,6 +286,11 @@ struct Slot {
 	const pech_desc *desc_view = nullptr; // device mapping of h_desc: the plan kernel reads it in place
 	uint32_t *h_out = nullptr, *d_out = nullptr;
 	uint32_t *out_view = nullptr; // device mapping of h_out: flat and direct launches store the results there
+	// a flat launch's status word (coherent pinned; layout.h PECH_FLAT_PUB /
+	// PECH_FLAT_ERR): checked before the results are taken (slot_verify)
+	uint64_t *h_stat = nullptr, *stat_view = nullptr;
+	uint64_t flat_tag = 0;  // the slot's flat launch (0: none)
+	bool published = false; // ... which stores the results in h_out itself
 	std::atomic<int> finished{0}; // set by the stream's host function after the results' D2H
 	std::atomic<int> waiting{0};  // a submit sleeps on `finished` (futex): the host function wakes it
 	int efd = -1;                 // the context's eventfd
@@ -345,6 +350,9 @@ struct crc32c_async {
 	uint64_t submitted = 0; // submissions accepted
 	uint64_t host_out = 0;  // launches whose results the kernel stored in h_out
 	uint64_t polled = 0;    // launches notified by the notifier thread
+	bool lone_taken = false;  // the messenger adapter host-routed a lone payload since the last flush
+	uint64_t faults = 0;      // flat launches whose results the kernel voided (their payloads failed, -EIO)
+	uint64_t pub_missing = 0; // flat launches whose in-kernel publication was missing (results copied instead)
 	// How a finished batch reaches the eventfd.  A host function on the
 	// slot's stream (hipLaunchHostFunc) sleeps until an interrupt, but the
 	// runtime takes ~10 us to run it: a lone 64 KiB payload waited 37.7 us
@@ -362,7 +370,7 @@ struct crc32c_async {
 	std::mutex nmu;
 	std::condition_variable ncv;
 	std::deque<Slot *> nq; // launched slots, in launch order
-	bool nstop = false;
+	std::atomic<bool> nstop{false};
 };
 
 static inline uint64_t thread_ns()
@@ -405,6 +413,8 @@ static void slot_free(Slot *s)
 		(void)hipFree(s->d_desc);
 	if (s->h_out)
 		(void)hipHostFree(s->h_out);
+	if (s->h_stat)
+		(void)hipHostFree(s->h_stat);
 	if (s->d_out)
 		(void)hipFree(s->d_out);
 	if (s->ev_done)
@@ -423,7 +433,8 @@ static Slot *slot_new(int efd)
 	    hipHostMalloc(&s->h_desc, kSlotDescs * sizeof(pech_desc), hipHostMallocDefault) != hipSuccess ||
 	    hipMalloc(&s->d_desc, kSlotDescs * sizeof(pech_desc)) != hipSuccess ||
 	    hipHostMalloc(&s->h_out, kSlotDescs * 4u, hipHostMallocDefault) != hipSuccess ||
-	    hipMalloc(&s->d_out, kSlotDescs * 4u) != hipSuccess) {
+	    hipMalloc(&s->d_out, kSlotDescs * 4u) != hipSuccess ||
+	    hipHostMalloc((void **)&s->h_stat, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
 		pech_internal_set_err("crc32c_async: slot allocation failed: %s", hipGetErrorString(hipGetLastError()));
 		slot_free(s);
 		return nullptr;
@@ -435,9 +446,15 @@ static Slot *slot_new(int efd)
 		s->desc_view = (const pech_desc *)dv;
 	else
 		(void)hipGetLastError(); // no mapping: descriptors go by H2D copy
+	memset(s->h_stat, 0, 64);
+	dv = nullptr;
+	if (hipHostGetDevicePointer(&dv, s->h_stat, 0) == hipSuccess && dv)
+		s->stat_view = (uint64_t *)dv;
+	else
+		(void)hipGetLastError(); // (no status word: flat launches then take the D2H copy, below)
 	const char *ho = getenv("PECH_ASYNC_HOST_OUT"); // A/B: 0 = results by D2H copy after every launch
 	dv = nullptr;
-	if (!(ho && ho[0] == '0') && hipHostGetDevicePointer(&dv, s->h_out, 0) == hipSuccess && dv)
+	if (!(ho && ho[0] == '0') && s->stat_view && hipHostGetDevicePointer(&dv, s->h_out, 0) == hipSuccess && dv)
 		s->out_view = (uint32_t *)dv;
 	else
 		(void)hipGetLastError();
@@ -497,6 +514,45 @@ static void harvest(crc32c_async *a, Slot *s, int err)
 }
 
 static int issue_slot(crc32c_async *a, Slot *s);
+
+// Before a finished slot's results are taken: a flat launch
+// reports in its status word whether one of its waves gave up waiting for
+// out[]'s initialisation (PECH_FLAT_ERR: the results are void -- the slot's
+// payloads fail with -EIO, and the messenger adapter recomputes them on the
+// host) and, when it was to store the results in h_out itself, that it did
+// (PECH_FLAT_PUB; missing: the results come from the device's out[] by a
+// copy).  Either way no CRC the kernel did not publish for this launch
+// reaches a callback.  Both are counted (crc32c_async_get_stats).
+static int slot_verify(crc32c_async *a, Slot *s)
+{
+	if (!s->flat_tag || !s->h_stat)
+		return 0;
+	const uint64_t v = __atomic_load_n(s->h_stat, __ATOMIC_ACQUIRE);
+	if (v == PECH_FLAT_ERR(s->flat_tag)) {
+		a->faults++;
+		pech_internal_set_err("crc32c_async: a flat launch voided its results (its wait for out[] timed out)");
+		return -EIO;
+	}
+	if (!s->published || v == PECH_FLAT_PUB(s->flat_tag))
+		return 0;
+	a->pub_missing++;
+	int cur = -1;
+	if (hipGetDevice(&cur) != hipSuccess)
+		cur = -1;
+	hipError_t e = hipSetDevice(a->dev);
+	if (e == hipSuccess)
+		e = hipMemcpyAsync(s->h_out, s->d_out, s->pieces.size() * 4u, hipMemcpyDeviceToHost, s->stream);
+	if (e == hipSuccess)
+		e = hipStreamSynchronize(s->stream);
+	if (cur >= 0)
+		(void)hipSetDevice(cur);
+	if (e != hipSuccess) {
+		pech_internal_set_err("crc32c_async: results copy after a missing publication failed: %s",
+				      hipGetErrorString(e));
+		return -EIO;
+	}
+	return 0;
+}
 
 // Harvest finished slots (blocking on the oldest when `wait`), in order.
 static int reap(crc32c_async *a, bool wait_oldest, DeviceGuard *dg = nullptr)
@@ -560,6 +616,8 @@ static int reap(crc32c_async *a, bool wait_oldest, DeviceGuard *dg = nullptr)
 			pech_internal_set_err("crc32c_async: batch failed: %s", hipGetErrorString(q));
 			err = -EIO;
 			a->err = err;
+		} else {
+			err = slot_verify(a, s); // (not sticky: the next batch is unaffected)
 		}
 		a->inflight.pop_front();
 		harvest(a, s, err);
@@ -648,7 +706,6 @@ static int issue_slot(crc32c_async *a, Slot *s)
 	ProfScope ps_copies(a, 0);
 	if (!s->dma.empty()) {
 		hipError_t e = hipErrorInvalidValue;
-		size_t from = 0; // first copy the per-copy fallback issues
 		if (!pech_fault(PECH_FAULT_ASYNC_DMA)) {
 			e = hipErrorNotSupported;
 			if (batch_copy_fn bc = batch_copy()) {
@@ -662,24 +719,26 @@ static int issue_slot(crc32c_async *a, Slot *s)
 				size_t fail_idx = SIZE_MAX;
 				e = bc(dsts.data(), srcs.data(), sizes.data(), dsts.size(), nullptr, nullptr, 0, &fail_idx,
 				       s->stream);
-				// copies before fail_idx are queued: the per-copy calls resume
-				// there, so none is issued twice
-				if (e != hipSuccess && fail_idx < s->dma.size())
-					from = fail_idx;
+				// On a failure the per-copy calls issue EVERY copy again, from
+				// copy 0: fail_idx only says where the batched call
+				// stopped, not that the copies before it were queued, and a copy
+				// never issued would leave stale staging bytes under a "good"
+				// CRC; issuing a copy twice on one stream is harmless (the same
+				// bytes land twice).
 				if (e != hipSuccess && e != hipErrorNotSupported && e != hipErrorInvalidValue) {
 					static std::once_flag warned;
 					const hipError_t e0 = e;
 					std::call_once(warned, [&] {
 						fprintf(stderr, "pech_crc32c: hipMemcpyBatchAsync failed at copy %zu: %s; "
-								"issuing the rest one call each\n",
-							from, hipGetErrorString(e0));
+								"issuing every copy again, one call each\n",
+							fail_idx, hipGetErrorString(e0));
 					});
 				}
 			}
 			if (e != hipSuccess) { // no batched call in this runtime (or it refused): one call each
 				(void)hipGetLastError();
 				e = hipSuccess;
-				for (size_t k = from; k < s->dma.size(); ++k) {
+				for (size_t k = 0; k < s->dma.size(); ++k) {
 					const DmaCopy &c = s->dma[k];
 					if ((e = hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyHostToDevice, s->stream)) !=
 					    hipSuccess)
@@ -713,9 +772,10 @@ static int issue_slot(crc32c_async *a, Slot *s)
 	// (rc 1: no copy after them -- a blit kernel and its dispatch, ~4-5 us of
 	// a lone payload's latency, profiles/r05/lat_prof.txt), else copied
 	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream,
-				      s->maxlen < kDirectMax && !a->planned_only, s->out_view);
+				      s->maxlen < kDirectMax && !a->planned_only, s->out_view, s->stat_view, &s->flat_tag);
 	if (rc < 0)
 		return fail_slot(a, s, rc);
+	s->published = rc == 1 && s->flat_tag != 0;
 	if (rc == 0)
 		TRY_HIP(hipMemcpyAsync(s->h_out, s->d_out, m * 4u, hipMemcpyDeviceToHost, s->stream),
 			fail_slot(a, s, -EIO));
@@ -813,6 +873,12 @@ static void notifier_main(crc32c_async *a)
 				}
 			}
 			while ((e = hipEventQuery(s->ev_done)) == hipErrorNotReady) {
+				// destroy: it has drained every slot before it asks
+				// the thread to stop, so a batch still polled then never
+				// completes (a failed stream's reap() already failed its
+				// payloads): give up on it rather than block the join
+				if (a->nstop.load(std::memory_order_relaxed))
+					break;
 				if (mono_ns() - t0 > 2 * s->est_ns + 100000u) {
 					struct timespec ts = {0, 20000};
 					nanosleep(&ts, nullptr);
@@ -862,8 +928,15 @@ static struct crc32c_async *async_create(unsigned int flags)
 		crc32c_async_destroy(a);
 		return nullptr;
 	}
-	if (a->notify)
-		a->notifier = std::thread(notifier_main, a);
+	if (a->notify) {
+		//  no exception may cross the C-ABI: without a thread
+		// every batch is notified by a host function (mode 0)
+		try {
+			a->notifier = std::thread(notifier_main, a);
+		} catch (...) {
+			a->notify = 0;
+		}
+	}
 	a->ready = true;
 	return a;
 }
@@ -919,6 +992,8 @@ extern "C" int crc32c_async_get_stats(const struct crc32c_async *a, struct crc32
 	st->launches = a->launches;
 	st->host_out = a->host_out;
 	st->polled = a->polled;
+	st->faults = a->faults;
+	st->pub_missing = a->pub_missing;
 	st->inflight = st->queued = 0;
 	for (const Slot *s : a->inflight)
 		(s->queued ? st->queued : st->inflight)++;
@@ -1033,10 +1108,25 @@ extern "C" int crc32c_async_submit(struct crc32c_async *a, const void *buf, unsi
 	return on_lib_stack([&] { return async_submit(a, buf, len, seed, done, arg); });
 }
 
+// The messenger adapter's queue-depth signal (crc32c_msgr.c route_host): a
+// payload is "lone" when nothing is outstanding on the context and no other
+// was taken as lone since the last flush -- the patched messenger flushes at
+// the end of every con_work pass, so a burst read in one pass sends its
+// first payload to the host and the rest to the GPU, while queue depth 1
+// (one message per pass) sends every one to the host.
+extern "C" PECH_HIDDEN int pech_async_take_lone(struct crc32c_async *a)
+{
+	if (!a || !a->items.empty() || a->lone_taken)
+		return 0;
+	a->lone_taken = true;
+	return 1;
+}
+
 extern "C" int crc32c_async_flush(struct crc32c_async *a)
 {
 	if (!a)
 		return -EINVAL;
+	a->lone_taken = false; // (a new pass: see pech_async_take_lone)
 	if (a->err)
 		return a->err;
 	if (!a->cur || a->cur->pieces.empty())

@@ -1573,6 +1573,37 @@ __device__ __forceinline__ bool prologue_flat(uint32_t *lds, const u32x4 (&dv)[4
 #define FLAT_INIT(tag) ((tag) << 1)
 #define FLAT_DONE(tag) (((tag) << 1) | 1ull)
 
+// The status word of a flat launch (hstat: coherent pinned host memory the
+// caller reads after the launch has completed; layout.h PECH_FLAT_PUB/ERR).
+// A wave that gave up waiting for out[]'s initialisation has XORed into
+// words that may not have been zeroed: it records the launch's tag in the
+// workspace's error word (ws word 2), counts the launch in pech_flat_faults
+// (first wave only) and stores PECH_FLAT_ERR(tag) to hstat, so no caller
+// takes the launch's results -- the library recomputes or fails the batch
+// (the reference cannot produce a wrong CRC, and a wrong one
+// would fault the connection: messenger.c:2826-2842).  The publisher of an
+// async slot's results (flat_publish) ends with PECH_FLAT_PUB(tag), or with
+// PECH_FLAT_ERR(tag) when the error word holds this launch's tag.
+__device__ unsigned long long pech_flat_faults;
+extern "C" int pech_read_flat_faults(uint64_t *host)
+{
+	return hipMemcpyFromSymbol(host, HIP_SYMBOL(pech_flat_faults), sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+__device__ __forceinline__ void flat_fault(uint64_t *flag, uint64_t *hstat, uint64_t tag, uint32_t lane)
+{
+	if (lane == 0) {
+		const uint64_t prev = atomicExch((unsigned long long *)(flag + 2), (unsigned long long)tag);
+		if (prev != tag)
+			atomicAdd(&pech_flat_faults, 1ull);
+		if (hstat)
+			__hip_atomic_store(hstat, PECH_FLAT_ERR(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+#ifdef PECH_DEBUG_BOUNDS
+	if (lane == 0)
+		printf("PECH OOB flat out[] never initialised blk %u\n", blockIdx.x);
+#endif
+}
+
 // Flat batches: the seed terms x^(8 len) s of R(s, D) = x^(8|D|) s ^ R(0, D),
 // and the seed itself for an empty buffer, XORed into out[] by the wave that
 // initialises it (the messenger's seeds are 0: nothing to do).
@@ -1623,16 +1654,22 @@ __device__ __forceinline__ void flat_init(const pech_desc *__restrict__ descs, u
 // consumed before the loop can exit, so no load of this rare path is left
 // pending at the step loop's join, where the compiler would wait for it with
 // a vmcnt(0), i.e. drain the ring at every step end.  (Bounded: a wave never
-// waits forever; ~1 s, then it goes on, and the bounds-checked build says so.)
+// waits forever; after ~1 s it records the launch as faulted (flat_fault)
+// and goes on, and no caller takes the launch's results.)  `test` (the
+// test library's fault hook, 0 from the release library):
+// PECH_FLAT_T_TIMEOUT makes every wave that reaches this wait take the
+// timeout at once.
 __device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &ready,
 					   const pech_desc *__restrict__ descs, uint32_t n, uint32_t lane,
-					   const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, bool seeds)
+					   const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, bool seeds,
+					   uint64_t *hstat, uint32_t test)
 {
 	if (ready)
 		return;
+	const bool force = test & PECH_FLAT_T_TIMEOUT;
 	for (uint32_t spin = 0;; ++spin) {
 		const uint64_t v = uni64(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-		if (v == FLAT_DONE(tag))
+		if (v == FLAT_DONE(tag) && !force)
 			break;
 		if ((v >> 1) != tag) { // no claim of this launch: claim it
 			uint64_t got = 0;
@@ -1644,11 +1681,8 @@ __device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &r
 			}
 			continue; // another wave claimed it first
 		}
-		if (spin >= (1u << 24)) {
-#ifdef PECH_DEBUG_BOUNDS
-			if (lane == 0)
-				printf("PECH OOB flat out[] never initialised blk %u\n", blockIdx.x);
-#endif
+		if (spin >= (1u << 24) || force) {
+			flat_fault(flag, hstat, tag, lane);
 			break;
 		}
 		__builtin_amdgcn_s_sleep(2); // FLAT_INIT: a running wave is at it
@@ -1672,8 +1706,16 @@ __device__ __forceinline__ void vm_done()
 {
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+// The results are followed by the launch's status word (hstat): the caller
+// takes hout only when it reads PECH_FLAT_PUB(tag) there, so a publication
+// that did not happen -- the nlive miscount of v0.32's first build, which
+// left 137 of 200 msgr_sim payloads with a previous batch's results -- is a
+// detected event, not stale CRCs.  The host reads hstat
+// after the launch has completed, which orders every store of the kernel.
+// (PECH_FLAT_T_NOPUB, test library only: the publication is skipped.)
 __device__ __forceinline__ void flat_publish(uint64_t *flag, uint32_t nlive, uint32_t n, uint32_t lane,
-					     uint32_t *__restrict__ out, uint32_t *__restrict__ hout)
+					     uint32_t *__restrict__ out, uint32_t *__restrict__ hout, uint64_t *hstat,
+					     uint64_t tag, uint32_t test)
 {
 	vm_done(); // (the flush's XORs; or, with nlive 0, flat_init's zeroes and seeds)
 	if (nlive) { // (0: a launch without rows, published by the wave that initialised out[])
@@ -1683,12 +1725,21 @@ __device__ __forceinline__ void flat_publish(uint64_t *flag, uint32_t nlive, uin
 		if (uni(c) + 1u != nlive)
 			return;
 	}
+	if (test & PECH_FLAT_T_NOPUB)
+		return;
 	asm volatile("" ::: "memory");
 #pragma unroll
 	for (uint32_t k = 0; k < PECH_FLAT_MAX / 64u; ++k) {
 		const uint32_t p = 64u * k + lane;
 		if (p < n)
 			hout[p] = __hip_atomic_load(out + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+	if (lane == 0 && hstat) {
+		// a wave of this launch that gave up on out[]'s initialisation has
+		// recorded the tag before it counted in (its own vm_done)
+		const uint64_t e = __hip_atomic_load(flag + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		__hip_atomic_store(hstat, e == tag ? PECH_FLAT_ERR(tag) : PECH_FLAT_PUB(tag), __ATOMIC_RELAXED,
+				   __HIP_MEMORY_SCOPE_SYSTEM);
 	}
 }
 
@@ -1698,7 +1749,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 					  const uint32_t *__restrict__ nzs, uint32_t n,
 					  const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint32_t rpw_min,
 					  const int64_t *__restrict__ deltas, const pech_desc *__restrict__ descs = nullptr,
-					  uint64_t *flag = nullptr, uint64_t tag = 0, uint32_t *__restrict__ hout = nullptr)
+					  uint64_t *flag = nullptr, uint64_t tag = 0, uint32_t *__restrict__ hout = nullptr,
+					  uint64_t *hstat = nullptr, uint32_t test = 0u)
 {
 	static_assert(!(FLAT && COPY), "flat batches: CRC only");
 	const uint32_t tid = threadIdx.x;
@@ -1874,7 +1926,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				__hip_atomic_store(flag, FLAT_DONE(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 		if (hout && Rtot == 0u && blockIdx.x == 0 && wave == 0) // no rows at all: out[] holds the seeds (flat_init above)
-			flat_publish(flag, 0u, n, lane, out, hout);
+			flat_publish(flag, 0u, n, lane, out, hout, hstat, tag, test);
 		if (!live)
 			return; // whole workgroup idle (small batch)
 		// Flat launches fill late at every size: with the wave-major shares of
@@ -2006,7 +2058,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	// (looked at only now, the flag's round trip hides behind the fill and
 	// the barrier)
 	if (FLAT && S.T)
-		ready = ready || uni64(seen) == FLAT_DONE(tag);
+		ready = ready || (uni64(seen) == FLAT_DONE(tag) && !(test & PECH_FLAT_T_TIMEOUT));
 	STAMP(t_start);
 	// the wave's first pool claim, one item ahead (resolved when its first
 	// item is done)
@@ -2241,7 +2293,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		tq[2] = __builtin_amdgcn_s_memrealtime();
 #endif
 		if (FLAT)
-			flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds);
+			flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds, hstat, test);
 		finish_run<!COPY>(lds, g8, s0, s1, s2, s3, step_m<FLAT>(S), STEP_RA(S), tpow, S.nu != 0, out, step_orig<FLAT>(S));
 		tpow = tpow_n;
 #ifdef PECH_STAMP_FIN
@@ -2268,7 +2320,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		static_assert(PECH_DEFER_SLOTS == 64u, "one slot per lane of the flushing wave");
 		if (done == PECH_MAIN_WAVES - 1u) {
 			if (FLAT)
-				flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds);
+				flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds, hstat, test);
 			const uint32_t k = lds[L_DEFER / 4u + lane];
 			bool flush = k != PECH_DEFER_EMPTY;
 #ifdef PECH_DEBUG_BOUNDS
@@ -2283,7 +2335,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #endif
 				atomicXor(out + k, lds[L_DEFER / 4u + PECH_DEFER_SLOTS + lane]);
 			if (FLAT && hout)
-				flat_publish(flag, sv.nlive, n, lane, out, hout);
+				flat_publish(flag, sv.nlive, n, lane, out, hout, hstat, tag, test);
 		}
 	}
 #ifdef PECH_STAMPS
@@ -2337,11 +2389,12 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_m
 // `tag` publish workgroup 0's zeroed out[] to the other workgroups.
 extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_flat(
 	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
-	uint32_t rpw_min, uint64_t *__restrict__ flag, uint64_t tag, uint32_t *__restrict__ hout)
+	uint32_t rpw_min, uint64_t *__restrict__ flag, uint64_t tag, uint32_t *__restrict__ hout, uint64_t *hstat,
+	uint32_t test)
 {
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	main_body<false, PECH_U, true>(lds, nullptr, nullptr, nullptr, nullptr, n, consts, out, rpw_min, nullptr, descs, flag,
-				       tag, hout);
+				       tag, hout, hstat, test);
 }
 
 // ---- direct kernel: small-buffer batches without a plan kernel -------------
@@ -2771,12 +2824,12 @@ extern "C" hipError_t pech_launch_main(uint32_t n, const pech_ws *ws, const uint
 // pech_launch_main; flag: 8-byte aligned device word, tag: fresh per launch
 extern "C" hipError_t pech_launch_flat(const pech_desc *descs, uint32_t n, const uint32_t *consts, uint32_t *out,
 				       uint32_t ncu, uint32_t rpw_min, uint64_t *flag, uint64_t tag, hipStream_t stream,
-				       hipEvent_t ev_start, hipEvent_t ev_stop, uint32_t *hout)
+				       hipEvent_t ev_start, hipEvent_t ev_stop, uint32_t *hout, uint64_t *hstat, uint32_t test)
 {
 	if (n == 0 || n > PECH_FLAT_MAX || ((uintptr_t)flag & 7u))
 		return hipErrorInvalidValue;
 	hipExtLaunchKernelGGL(pech_crc32c_flat, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u, descs,
-			      n, consts, out, rpw_min, flag, tag, hout);
+			      n, consts, out, rpw_min, flag, tag, hout, hstat, test);
 	return hipGetLastError();
 }
 
@@ -2799,6 +2852,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.32 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) " direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.33 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

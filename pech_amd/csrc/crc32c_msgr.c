@@ -11,6 +11,18 @@
  * once and takes the same queue/footer path as a GPU payload, so the
  * messenger's sequencing does not depend on the route.
  *
+ * Routing by queue depth: a payload of at most
+ * crc32c_msgr_set_lone_max() bytes (default PECH_MSGR_LONE_MAX_DEFAULT) that
+ * arrives while its context has nothing outstanding, and is the first such
+ * since the context's last flush (pech at queue depth 1: one
+ * read_partial_msg_data -> footer compare per con_work pass,
+ * messenger.c:2649-2684; the patch flushes at the end of every pass), is
+ * checksummed on the host too: alone, it cannot share a launch, so the GPU
+ * route costs the thread ~10 us of submit / launch / complete and the
+ * payload ~25-50 us of latency, which the host routine beats up to a few
+ * hundred KiB.  The payloads after it in the same pass --
+ * a burst -- batch on the GPU as before (throughput mode).
+ *
  * A GPU failure never reaches the messenger as a wrong or missing CRC: a
  * submission the async layer refuses, or a batch that fails, is recomputed
  * on the host from the same bytes, which the adapter still owns at that point.
@@ -28,8 +40,12 @@
 
 #define PECH_HIDDEN __attribute__((visibility("hidden")))
 PECH_HIDDEN uint32_t pech_cpu_crc32c(uint32_t crc, const void *data, size_t n);
+/* crc32c_async.cpp: 1 (and taken) when the context has nothing outstanding
+ * and no lone payload was host-routed since its last flush */
+PECH_HIDDEN int pech_async_take_lone(struct crc32c_async *a);
 
 #define PECH_MSGR_HOST_MAX_DEFAULT (8u << 10) /* profiles/r03/msgr_cutoff.txt */
+#define PECH_MSGR_LONE_MAX_DEFAULT (256u << 10) /* lone payloads: thread CPU crossover, DESIGN.md §6.7 */
 #define TX_BUCKETS 64u /* per connection, chained by msg address */
 
 enum { ST_WAIT, ST_DONE };
@@ -77,20 +93,36 @@ struct crc32c_msgr_conn {
 static struct crc32c_msgr_stats g_st;
 static unsigned int g_host_max = PECH_MSGR_HOST_MAX_DEFAULT;
 static int g_host_max_env;
+static unsigned int g_lone_max = PECH_MSGR_LONE_MAX_DEFAULT;
+static int g_lone_max_env;
+
+/* a byte count from the environment (once), else *v unchanged */
+static void env_bytes(const char *name, unsigned int *v, int *read)
+{
+	const char *e;
+
+	if (*read)
+		return;
+	*read = 1;
+	e = getenv(name);
+	if (e && *e) {
+		char *end = NULL;
+		const unsigned long long x = strtoull(e, &end, 0);
+		if (end != e)
+			*v = x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (unsigned int)x;
+	}
+}
 
 static unsigned int host_max(void)
 {
-	if (!g_host_max_env) {
-		const char *e = getenv("PECH_CRC32C_MSGR_HOST_MAX");
-		g_host_max_env = 1;
-		if (e && *e) {
-			char *end = NULL;
-			const unsigned long long v = strtoull(e, &end, 0);
-			if (end != e)
-				g_host_max = v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (unsigned int)v;
-		}
-	}
+	env_bytes("PECH_CRC32C_MSGR_HOST_MAX", &g_host_max, &g_host_max_env);
 	return g_host_max;
+}
+
+static unsigned int lone_max(void)
+{
+	env_bytes("PECH_CRC32C_MSGR_LONE_MAX", &g_lone_max, &g_lone_max_env);
+	return g_lone_max;
 }
 
 unsigned int crc32c_msgr_set_host_max(unsigned int bytes)
@@ -99,6 +131,29 @@ unsigned int crc32c_msgr_set_host_max(unsigned int bytes)
 
 	g_host_max = bytes;
 	return prev;
+}
+
+unsigned int crc32c_msgr_set_lone_max(unsigned int bytes)
+{
+	const unsigned int prev = lone_max();
+
+	g_lone_max = bytes;
+	return prev;
+}
+
+/* the route of one checked payload: 1 = host routine now (counted in *lone
+ * when only because its context is idle), 0 = the GPU */
+static int route_host(const struct crc32c_msgr_conn *c, unsigned int len, uint64_t *lone)
+{
+	if (!host_max())
+		return 0; /* 0: every checked payload to the GPU (lone ones too) */
+	if (len <= host_max())
+		return 1;
+	if (lone_max() && len <= lone_max() && pech_async_take_lone(c->a)) {
+		(*lone)++;
+		return 1;
+	}
+	return 0;
 }
 
 static void kick(struct crc32c_msgr_conn *c)
@@ -210,7 +265,7 @@ int crc32c_msgr_rx_queue(struct crc32c_msgr_conn *c, void *msg, const void *data
 		g_st.rx_unchecked++;
 		return 0;
 	}
-	if (host_max() && len <= host_max()) { /* small payload: the host routine is cheaper than a GPU round trip */
+	if (route_host(c, len, &g_st.rx_lone)) { /* small or lone payload: the host routine is cheaper */
 		g_st.rx_host++;
 		e->got = pech_cpu_crc32c(0, data, len);
 		e->state = ST_DONE;
@@ -354,7 +409,7 @@ int crc32c_msgr_tx_submit(struct crc32c_msgr_conn *c, void *msg, const void *dat
 	e->len = len;
 	e->seed = seed;
 	e->state = ST_WAIT;
-	if (host_max() && len <= host_max()) {
+	if (route_host(c, len, &g_st.tx_lone)) {
 		g_st.tx_host++;
 		e->crc = pech_cpu_crc32c(seed, data, len);
 		e->state = ST_DONE;

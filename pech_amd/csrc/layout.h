@@ -155,13 +155,29 @@ LAYOUT_FN uint32_t pech_size_class(uint32_t rows)
  *   deltas   i64[slots]              fused copy: destination - source per buffer
  * slots = nch * PECH_CHUNK, nch = ceil(m / PECH_CHUNK).
  * A flat launch (m <= PECH_FLAT_MAX, no plan kernel) uses only the first
- * 8 bytes: the u64 word through which its workgroup 0 publishes the zeroed
- * out[] (crc32c_kernels.hip, pech_crc32c_flat). */
+ * PECH_FLAT_WS_BYTES bytes, three u64 words (crc32c_kernels.hip,
+ * pech_crc32c_flat): [0] the claim/publication word of out[]'s
+ * initialisation (tag << 1 | done), [1] (low half) the count of workgroups
+ * done before an async slot's results are published, [2] the tag of a launch
+ * one of whose waves gave up waiting for out[] (its results are void). */
 struct pech_ws {
 	struct pech_core *cores;
 	uint32_t *lrs, *partials, *nzs;
 	int64_t *deltas;
 };
+
+#define PECH_FLAT_WS_BYTES 24u
+
+/* A flat launch's status word (hstat, coherent pinned host memory, read by
+ * the library after the launch has completed): PECH_FLAT_PUB(tag) once an
+ * async slot's results are stored in its host array, PECH_FLAT_ERR(tag) when
+ * a wave's wait for out[]'s initialisation timed out (the results are void);
+ * anything else is an earlier launch's word.  Tags are below 2^62. */
+#define PECH_FLAT_PUB(tag) (((uint64_t)(tag) << 2) | 1u)
+#define PECH_FLAT_ERR(tag) (((uint64_t)(tag) << 2) | 2u)
+/* test library only (crc32c_test_inject): the kernel's fault bits */
+#define PECH_FLAT_T_TIMEOUT 1u /* every wave that waits for out[] times out at once */
+#define PECH_FLAT_T_NOPUB 2u   /* the async slot's publication is skipped */
 
 static inline size_t pech_ws_align(size_t x) { return (x + 255u) & ~(size_t)255u; }
 
@@ -171,6 +187,10 @@ static inline size_t pech_ws_bytes(uint32_t m)
 	return pech_ws_align(slots * sizeof(struct pech_core)) + pech_ws_align(slots * 4u) +
 	       2u * pech_ws_align(PECH_MAX_CHUNKS * 4u) + pech_ws_align(slots * 8u);
 }
+
+#if defined(__cplusplus) && __cplusplus >= 201103L
+static_assert(PECH_FLAT_WS_BYTES <= 256u, "the flat words fit the first aligned array of any workspace");
+#endif
 
 static inline struct pech_ws pech_ws_carve(void *base, uint32_t m)
 {

@@ -129,6 +129,8 @@ static struct {
 	long revoke_polls, revoke_out_seen; /* revoke: polls of con->out_msg, distinct messages seen in it */
 	struct ceph_msg *revoke_target;     /* revoke: the message to revoke mid-send */
 	int revoke_queued, revoked_held;
+	int revoke_armed;                   /* revoke: the target's send is held (below) until it is revoked */
+	long held_writes, held_completes;   /* revoke: data writes / complete() calls held back */
 	struct work_struct revoke_work;
 	int ret;
 } S;
@@ -455,6 +457,57 @@ struct crc32c_async *__wrap_crc32c_async_create_on(int device, unsigned int flag
 	return a;
 }
 
+/* ---- the target held in place until it is revoked ------
+ * The revoke must land while the target is being sent; a poll racing the
+ * socket writes could miss that window on a loaded host.  So the harness
+ * holds the send itself:
+ *   inline (no async context): the client socket's writes of the target's
+ *   data report a full socket (-EAGAIN: ceph_tcp_sendiov returns 0 and the
+ *   messenger waits for write space) while it is con->out_msg and not yet
+ *   revoked, its header and front already sent -- the poll below always
+ *   finds it there;
+ *   adapter (async contexts): complete() delivers nothing while the target
+ *   is con->out_msg and not yet revoked, so its GPU CRC cannot be ready at
+ *   its footer -- the footer is held (tx_footer returns 0) and the work
+ *   item above revokes it there.
+ * Both end with the revoke; the hold cannot outlive it. */
+static int lb_holding(void)
+{
+	int i;
+
+	if (!S.revoke_armed || !S.revoke_target || S.ccon.out_msg != S.revoke_target)
+		return 0;
+	for (i = 0; i < S.nreq; i++)
+		if (S.req[i].m == S.revoke_target)
+			return !S.req[i].revoked;
+	return 0;
+}
+
+int __real_sock_sendmsg(struct socket *sock, struct kmsghdr *kmsg);
+
+/* the messenger's socket writes; held: the target's data pages
+ * (ceph_tcp_sendiov over the bvec, write_partial_message_data), once its
+ * header and front are on the wire */
+int __wrap_sock_sendmsg(struct socket *sock, struct kmsghdr *kmsg)
+{
+	if (S.nctx == 0 && sock == S.ccon.sock && iov_iter_is_bvec(&kmsg->msg_iter) && lb_holding()) {
+		S.held_writes++;
+		return -EAGAIN;
+	}
+	return __real_sock_sendmsg(sock, kmsg);
+}
+
+int __real_crc32c_async_complete(struct crc32c_async *a);
+
+int __wrap_crc32c_async_complete(struct crc32c_async *a)
+{
+	if (S.nctx > 0 && lb_holding()) {
+		S.held_completes++;
+		return 0;
+	}
+	return __real_crc32c_async_complete(a);
+}
+
 static void revoke_workfn(struct work_struct *w)
 {
 	struct lb_req *r;
@@ -579,8 +632,11 @@ static int lb_task(void *arg)
 		/* revoke_idx while it is being written (con->out_msg: its data on
 		 * the wire, or its footer held for the GPU CRC): the rest goes out
 		 * as zeros (write_partial_skip), the server faults on it, and the
-		 * client reconnects and resends everything else.  A message that
-		 * could not be caught mid-send is not revoked, and the run fails. */
+		 * client reconnects and resends everything else.  The harness holds
+		 * the target's send until then (lb_holding), so the revoke always
+		 * lands mid-send: inline from this poll, with the adapter from the
+		 * held footer's work item (this poll leaves that case to it). */
+		S.revoke_armed = 1;
 		while (!revoked_mid && !S.revoked_held && time_before(jiffies, deadline) &&
 		       !S.req[revoke_idx].srv_seen && !S.req[revoke_idx].replied) {
 			S.revoke_polls++;
@@ -588,7 +644,7 @@ static int lb_task(void *arg)
 				last_out = S.ccon.out_msg;
 				S.revoke_out_seen++;
 			}
-			if (S.ccon.out_msg == S.req[revoke_idx].m) {
+			if (S.nctx == 0 && S.ccon.out_msg == S.req[revoke_idx].m) {
 				S.req[revoke_idx].revoked = 1;
 				ceph_msg_revoke(S.req[revoke_idx].m);
 				revoked_mid = 1;
@@ -652,7 +708,7 @@ static int lb_task(void *arg)
 		       "\"revoked_footer_held\": %d, "
 		       "\"srv_dispatched\": %d, \"srv_dups\": %d, \"cli_dispatched\": %d, \"cli_dups\": %d, "
 		       "\"pings_skipped\": %d, \"srv_faults\": %d, \"cli_faults\": %d, \"cli_resent\": %d, "
-		       "\"revoke_polls\": %ld, \"revoke_out_seen\": %ld, "
+		       "\"revoke_polls\": %ld, \"revoke_out_seen\": %ld, \"held_writes\": %ld, \"held_completes\": %ld, "
 		       "\"relay_conns\": %d, \"relay_flips\": %d, \"bad_bytes\": %d, \"bad_footer\": %d, "
 		       "\"bad_order\": %d, \"bad_front\": %d, \"msgs_alloc\": %ld, \"msgs_freed\": %ld, "
 		       "\"adapter\": {\"rx_submitted\": %llu, \"rx_host\": %llu, \"rx_unchecked\": %llu, "
@@ -661,7 +717,7 @@ static int lb_task(void *arg)
 		       S.scenario, ok ? "true" : "false", S.nreq, unanswered, revoked_mid, S.revoked_held, S.srv_dispatched,
 		       S.srv_dups,
 		       S.cli_dispatched, S.cli_dups, S.pings, S.srv_faults, S.cli_faults, S.cli_resent,
-		       S.revoke_polls, S.revoke_out_seen, lb_proxy_conns(), lb_proxy_flips(), S.bad_bytes, S.bad_footer, S.bad_order, S.bad_front,
+		       S.revoke_polls, S.revoke_out_seen, S.held_writes, S.held_completes, lb_proxy_conns(), lb_proxy_flips(), S.bad_bytes, S.bad_footer, S.bad_order, S.bad_front,
 		       S.msgs_alloc, S.msgs_freed, (unsigned long long)st.rx_submitted,
 		       (unsigned long long)st.rx_host, (unsigned long long)st.rx_unchecked,
 		       (unsigned long long)st.rx_verified, (unsigned long long)st.rx_bad,

@@ -120,10 +120,13 @@ def build_loopback(out):
                 raise RuntimeError(r.stderr[-3000:])
         os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
         tmp = out + ".tmp"
-        # the test wraps the messenger's held-footer call (revoke scenario)
-        # and its context creation (the contexts' counters)
+        # the test wraps the messenger's held-footer call, its socket
+        # writes and its complete() calls (the revoke scenario holds the
+        # target's send until it is revoked) and its context creation (the
+        # contexts' counters)
         r = subprocess.run(["gcc", "-o", tmp, lb, px, orc, *objs, *LINK_LIBS, "-Wl,-rpath,$ORIGIN/../pech_amd",
-                            "-Wl,--wrap=crc32c_msgr_tx_footer", "-Wl,--wrap=crc32c_async_create_on"],
+                            "-Wl,--wrap=crc32c_msgr_tx_footer", "-Wl,--wrap=crc32c_async_create_on",
+                            "-Wl,--wrap=sock_sendmsg", "-Wl,--wrap=crc32c_async_complete"],
                            capture_output=True, text=True, timeout=300)
         if r.returncode:
             raise RuntimeError(r.stderr[-3000:])

@@ -294,3 +294,104 @@ def test_msgr_connection_state_machine(mode, corrupt, host_max):
             assert rx_host == 0 and tx_host == 0
         else:  # 0/1/100/4096/4097-byte payloads stayed on the host
             assert rx_host > 0 and tx_host > 0
+
+
+@pytest.mark.gpu
+def test_msgr_lone_payloads_route_to_the_host():
+    """Routing by queue depth (VERDICT r05 #4, crc32c_msgr.c route_host): a
+    payload of at most crc32c_msgr_set_lone_max() bytes that finds its
+    context idle, the first since the last flush, is checksummed on the host
+    (rx_lone / tx_lone); the rest of a burst read in the same pass goes to
+    the GPU; payloads above the cutoff always do; host_max 0 sends
+    everything to the GPU.  Every CRC checked against the oracle."""
+    import ctypes
+
+    import pech_amd as P
+    from pech_amd import _lib
+
+    L = _lib.lib()
+    released = []
+    REL = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    rel = REL(lambda m: released.append(m))
+    ac = P.AsyncCrc()
+    conn = L.crc32c_msgr_conn_create(ac.handle, 64, None, None, ctypes.cast(rel, ctypes.c_void_p))
+    assert conn
+    rng = np.random.default_rng(61)
+    bufs = [rng.integers(0, 256, n, dtype=np.uint8) for n in (65536, 65536, 65536, 65536, 200000, 1 << 20, 65536)]
+    want = [O.crc(0, b) for b in bufs]
+
+    def st():
+        s = _lib.CMsgrStats()
+        L.crc32c_msgr_get_stats(ctypes.byref(s))
+        return {k: int(getattr(s, k)) for k, _ in _lib.CMsgrStats._fields_}
+
+    def queue(i):
+        assert L.crc32c_msgr_rx_queue(conn, ctypes.c_void_p(0x1000 + i), bufs[i].ctypes.data, bufs[i].size, 1,
+                                      want[i]) == 0
+
+    def take(n):
+        got = []
+        for _ in range(4000):
+            L.crc32c_async_complete(ac.handle)
+            m, c = ctypes.c_void_p(), ctypes.c_uint32()
+            while len(got) < n:
+                rc = L.crc32c_msgr_rx_next(conn, ctypes.byref(m), ctypes.byref(c))
+                if rc != 1:
+                    assert rc == 0, rc
+                    break
+                got.append((m.value - 0x1000, c.value))
+            if len(got) == n:
+                return got
+            select.select([ac.fd()], [], [], 0.005)
+        raise AssertionError(f"{n - len(got)} payload(s) never completed")
+
+    prev_host = L.crc32c_msgr_set_host_max(8192)
+    prev_lone = L.crc32c_msgr_set_lone_max(256 << 10)
+    try:
+        L.crc32c_async_flush(ac.handle)
+        s0 = st()
+        queue(0)  # queue depth 1: lone -> host
+        assert take(1) == [(0, want[0])]
+        L.crc32c_async_flush(ac.handle)
+        s1 = st()
+        assert s1["rx_lone"] == s0["rx_lone"] + 1 and s1["rx_host"] == s0["rx_host"] + 1
+        assert s1["rx_submitted"] == s0["rx_submitted"]
+        for i in (1, 2, 3, 4):  # a burst in one pass: the first lone, the rest batch on the GPU
+            queue(i)
+        L.crc32c_async_flush(ac.handle)
+        assert take(4) == [(i, want[i]) for i in (1, 2, 3, 4)]
+        s2 = st()
+        assert s2["rx_lone"] == s1["rx_lone"] + 1 and s2["rx_submitted"] == s1["rx_submitted"] + 3, (s1, s2)
+        queue(5)  # 1 MiB: above the lone cutoff, GPU even when idle
+        L.crc32c_async_flush(ac.handle)
+        assert take(1) == [(5, want[5])]
+        s3 = st()
+        assert s3["rx_lone"] == s2["rx_lone"] and s3["rx_submitted"] == s2["rx_submitted"] + 1
+        L.crc32c_msgr_set_host_max(0)  # everything to the GPU, lone payloads too
+        queue(6)
+        L.crc32c_async_flush(ac.handle)
+        assert take(1) == [(6, want[6])]
+        s4 = st()
+        assert s4["rx_lone"] == s3["rx_lone"] and s4["rx_submitted"] == s3["rx_submitted"] + 1
+        L.crc32c_msgr_set_host_max(8192)
+        # send side: a lone message's footer is ready at once (host), the
+        # next one in the same pass is submitted
+        crc = ctypes.c_uint32()
+        assert L.crc32c_msgr_tx_submit(conn, ctypes.c_void_p(0x77), bufs[0].ctypes.data, bufs[0].size, 0) == 0
+        assert L.crc32c_msgr_tx_submit(conn, ctypes.c_void_p(0x78), bufs[1].ctypes.data, bufs[1].size, 0) == 0
+        s5 = st()
+        assert s5["tx_lone"] == s4["tx_lone"] + 1 and s5["tx_submitted"] == s4["tx_submitted"] + 1
+        assert L.crc32c_msgr_tx_footer(conn, ctypes.c_void_p(0x77), ctypes.byref(crc)) == 1 and crc.value == want[0]
+        L.crc32c_async_flush(ac.handle)
+        for _ in range(4000):
+            L.crc32c_async_complete(ac.handle)
+            if L.crc32c_msgr_tx_footer(conn, ctypes.c_void_p(0x78), ctypes.byref(crc)) == 1:
+                break
+            select.select([ac.fd()], [], [], 0.005)
+        assert crc.value == want[1]
+    finally:
+        L.crc32c_msgr_set_host_max(prev_host)
+        L.crc32c_msgr_set_lone_max(prev_lone)
+        L.crc32c_msgr_conn_destroy(conn)
+        ac.close()
+    assert released == []

@@ -22,8 +22,10 @@ def run(*extra):
 
 
 def test_single_thread_matches_process_per_gpu_schema():
-    a = run()
-    b = run("--single-thread", "--gpus", "1")
+    # 30-step passes for the agreement check below (6-step passes are ~1 ms
+    # of GPU time, where the Python loop's jitter shows)
+    a = run("--steps", "30")
+    b = run("--single-thread", "--gpus", "1", "--steps", "30")
     c = run("--single-thread", "--devices", "0,0")
     assert set(a) == set(b) and set(a["roofline"]) == set(b["roofline"])
     assert set(c) - set(a) == {"shards_checked", "buffers_checked"} and c["shards_checked"] == 2
@@ -31,10 +33,13 @@ def test_single_thread_matches_process_per_gpu_schema():
     assert c["buffers_checked"] == 2 * c["config"]["buffers_per_gpu"] * 2
     assert a["n_gpus"] == b["n_gpus"] == c["n_gpus"] == 1
     assert "single-thread" in b["config"]["parallelism"] and "single-thread" in c["config"]["parallelism"]
-    # same work on one GPU: the two drivers agree (the bench log records ~1-2 %
-    # at 50 steps; these are 6-step passes, and the bounds-checked build's
-    # launches vary more: 12 % apart once in round 5)
-    assert abs(a["value"] - b["value"]) / a["value"] < 0.20, (a["value"], b["value"])
+    # same work on one GPU: the two drivers agree within 10 % (VERDICT r05 #7,
+    # ADVICE r5): per launch (the same kernels) and on the one-stream pass
+    # (the host's issue loop included), each over 30 steps
+    ka, kb = a["roofline"]["avg_launch_us"], b["roofline"]["avg_launch_us"]
+    assert abs(ka - kb) / ka < 0.10, (ka, kb)
+    sa, sb = a["serial"]["value"], b["serial"]["value"]
+    assert abs(sa - sb) / sa < 0.10, (sa, sb)
     # two shards on one GPU share its HBM: about one GPU's rate in aggregate
     assert 0.7 < c["value"] / a["value"] < 1.3, (a["value"], c["value"])
 

@@ -15,7 +15,11 @@ each test below checks its scenario's outcome:
   one whose own submit filled the slot and whose launch failed (under the
   messenger adapter too: no callback reaches a freed verify-queue entry);
 * a batch whose stream fails after its launch never signals the eventfd;
-  complete() finds it by asking the stream and fails its payloads.
+  complete() finds it by asking the stream and fails its payloads;
+* a flat launch whose waves gave up waiting for out[]'s initialisation, or
+  whose async results publication is missing, never hands out a CRC: the
+  drop-in recomputes, crc32c_batch fails, the async slot fails (-EIO) or
+  copies the results, the adapter recomputes; all counted.
 Run on the GPU box (-m gpu)."""
 import ctypes
 import json
@@ -31,6 +35,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TEST_LIB = os.path.join(REPO, "build", "lib_test.so")
 SITE_DROPIN_GPU, SITE_ASYNC_LAUNCH, SITE_ASYNC_DMA, SITE_ASYNC_STREAM = 0, 1, 2, 3
+SITE_FLAT_TIMEOUT, SITE_FLAT_NOPUB = 4, 5  # the flat kernel's fault bits (layout.h PECH_FLAT_T_*)
 SLOT_DESCS, SLOT_BYTES = 8192, 32 << 20  # crc32c_async.cpp kSlotDescs / kSlotBytes
 
 
@@ -44,7 +49,8 @@ def inject(site, countdown):
 
 
 def disarm():
-    for s in (SITE_DROPIN_GPU, SITE_ASYNC_LAUNCH, SITE_ASYNC_DMA, SITE_ASYNC_STREAM):
+    for s in (SITE_DROPIN_GPU, SITE_ASYNC_LAUNCH, SITE_ASYNC_DMA, SITE_ASYNC_STREAM, SITE_FLAT_TIMEOUT,
+              SITE_FLAT_NOPUB):
         inject(s, 0)
 
 
@@ -298,6 +304,177 @@ def sc_failed_stream_found_by_blocked_submit():
         assert got[i] == (O.crc(i, bufs[i]), 0), (i, got.get(i))
     assert 4 not in got and ac.pending() == 0 and ac.stray == 0
     ac.close()
+
+
+# ---- flat launches that void or miss their results ---------
+# The test library arms the flat kernel's own fault bits (layout.h
+# PECH_FLAT_T_*): every wave that waits for out[]'s initialisation times out
+# at once (its results are void and the kernel reports PECH_FLAT_ERR), or the
+# async slot's in-kernel publication is skipped.  No wrong CRC may reach a
+# caller: the drop-in recomputes on the host, crc32c_batch fails loudly, the
+# async layer fails the slot's payloads (-EIO, not sticky) or copies the
+# results from the GPU, the adapter recomputes on the host; every event is
+# counted.
+def _big_payloads(rng, k, size=1 << 20):
+    return [rng.integers(0, 256, size + 977 * i, dtype=np.uint8) for i in range(k)]
+
+
+def sc_flat_timeout_dropin_recomputed_on_host():
+    import oracle_lib as O
+    import pech_amd as P
+
+    rng = np.random.default_rng(51)
+    prev = P.set_cpu_max(0)  # every call through the GPU: > 64 KiB is one flat launch
+    try:
+        d = rng.integers(0, 256, 300000, dtype=np.uint8)
+        before = P.stats()
+        assert P.crc32c(5, d) == O.crc(5, d)
+        inject(SITE_FLAT_TIMEOUT, 1)
+        assert P.crc32c(6, d) == O.crc(6, d)  # voided on the GPU, recomputed on the host
+        assert P.crc32c(7, d) == O.crc(7, d)
+        after = P.stats()
+        assert after["gpu_faults"] == before["gpu_faults"] + 1, (before, after)
+        assert after["gpu_fallbacks"] == before["gpu_fallbacks"] + 1, (before, after)
+        assert after["gpu_calls"] == before["gpu_calls"] + 2, (before, after)
+    finally:
+        P.set_cpu_max(prev)
+
+
+def sc_flat_timeout_batch_fails_loudly():
+    import oracle_lib as O
+    import pech_amd as P
+    import torch
+
+    rng = np.random.default_rng(52)
+    bufs = _big_payloads(rng, 5)
+    want = [O.crc(0, b) for b in bufs]
+    assert P.crc32c_batch([b.tobytes() for b in bufs]) == want
+    before = P.stats()
+    inject(SITE_FLAT_TIMEOUT, 1)
+    try:
+        P.crc32c_batch([b.tobytes() for b in bufs])
+        raise AssertionError("crc32c_batch returned results of a voided flat launch")
+    except P.Crc32cError:
+        pass
+    assert P.crc32c_batch([b.tobytes() for b in bufs]) == want  # the next call is exact
+    # a device entry point's caller reads the fault from the counters
+    dev = torch.device("cuda", 0)
+    t = [torch.from_numpy(b).to(dev) for b in bufs]
+    descs = P.make_descs([x.data_ptr() for x in t], [x.numel() for x in t], device=dev)
+    out = torch.zeros(len(t), dtype=torch.int32, device=dev)
+    ws = torch.empty(P.workspace_bytes(len(t)), dtype=torch.uint8, device=dev)
+    inject(SITE_FLAT_TIMEOUT, 1)
+    P.dev_batch_ws_async(descs, out, ws)
+    torch.cuda.synchronize()
+    mid = P.stats()
+    assert mid["gpu_faults"] == before["gpu_faults"] + 2, (before, mid)
+    P.dev_batch_ws_async(descs, out, ws)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().view(np.uint32).tolist() == want
+    assert P.stats()["gpu_faults"] == mid["gpu_faults"]
+
+
+def sc_flat_timeout_async_slot_fails_not_sticky():
+    import oracle_lib as O
+    import pech_amd as P
+
+    rng = np.random.default_rng(53)
+    bufs = _big_payloads(rng, 6)
+    ac = P.AsyncCrc()
+    got = {}
+    cb = lambda i: (lambda crc, err: got.__setitem__(i, (crc, err)))  # noqa: E731
+    for i in (0, 1):  # one flat batch, exact
+        ac.submit(bufs[i].ctypes.data, bufs[i].size, i, cb(i), keep=bufs[i])
+    ac.drain()
+    s0 = ac.stats()
+    inject(SITE_FLAT_TIMEOUT, 1)
+    for i in (2, 3):  # its batch is voided by the kernel: err < 0, no CRC
+        ac.submit(bufs[i].ctypes.data, bufs[i].size, i, cb(i), keep=bufs[i])
+    try:
+        ac.drain()
+    except P.Crc32cError:
+        pass
+    for i in (4, 5):  # not sticky: the next batch is exact
+        ac.submit(bufs[i].ctypes.data, bufs[i].size, i, cb(i), keep=bufs[i])
+    ac.drain()
+    s1 = ac.stats()
+    for i in (0, 1, 4, 5):
+        assert got[i] == (O.crc(i, bufs[i]), 0), (i, got.get(i))
+    assert got[2][1] < 0 and got[3][1] < 0, got
+    assert s1["faults"] == s0["faults"] + 1 and s1["pub_missing"] == s0["pub_missing"], (s0, s1)
+    assert ac.pending() == 0 and ac.stray == 0
+    ac.close()
+
+
+def sc_flat_missing_publication_never_stale():
+    # the slot's host array still holds the previous batch's results when
+    # the publication is skipped: the callbacks must get THIS batch's CRCs
+    import oracle_lib as O
+    import pech_amd as P
+
+    rng = np.random.default_rng(54)
+    bufs = _big_payloads(rng, 4)
+    ac = P.AsyncCrc()
+    got = {}
+    cb = lambda i: (lambda crc, err: got.__setitem__(i, (crc, err)))  # noqa: E731
+    for i in (0, 1):
+        ac.submit(bufs[i].ctypes.data, bufs[i].size, i, cb(i), keep=bufs[i])
+    ac.drain()
+    s0 = ac.stats()
+    inject(SITE_FLAT_NOPUB, 1)
+    for i in (2, 3):  # same slot, same piece count: h_out holds batch 1's words
+        ac.submit(bufs[i].ctypes.data, bufs[i].size, i, cb(i), keep=bufs[i])
+    ac.drain()
+    s1 = ac.stats()
+    for i in range(4):
+        assert got[i] == (O.crc(i, bufs[i]), 0), (i, got.get(i))
+    assert s1["pub_missing"] == s0["pub_missing"] + 1 and s1["faults"] == s0["faults"], (s0, s1)
+    assert s1["host_out"] >= s0["host_out"] + 1, (s0, s1)  # it was a publishing flat launch
+    ac.close()
+
+
+def sc_flat_timeout_under_the_adapter_is_recomputed():
+    # the messenger adapter (crc32c_msgr.c) gets err < 0 for a voided batch
+    # and checksums the payload on the host: the footer compare still sees
+    # the exact CRC (rx_verified, no rx_bad)
+    import oracle_lib as O
+    import pech_amd as P
+    from pech_amd import _lib
+
+    L = _lib.lib()
+    prev = L.crc32c_msgr_set_host_max(0)
+    released = []
+    REL = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    rel = REL(lambda m: released.append(m))
+    ac = P.AsyncCrc()
+    conn = L.crc32c_msgr_conn_create(ac.handle, 16, None, None, ctypes.cast(rel, ctypes.c_void_p))
+    assert conn
+    try:
+        rng = np.random.default_rng(55)
+        big = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+        want = O.crc(0, big)
+        st0 = _lib.CMsgrStats()
+        L.crc32c_msgr_get_stats(ctypes.byref(st0))
+        inject(SITE_FLAT_TIMEOUT, 1)
+        assert L.crc32c_msgr_rx_queue(conn, ctypes.c_void_p(9), big.ctypes.data, big.size, 1, want) == 0
+        L.crc32c_async_flush(ac.handle)
+        msg, crc = ctypes.c_void_p(), ctypes.c_uint32()
+        for _ in range(2000):
+            L.crc32c_async_complete(ac.handle)
+            if L.crc32c_msgr_rx_next(conn, ctypes.byref(msg), ctypes.byref(crc)) == 1:
+                break
+            select.select([ac.fd()], [], [], 0.01)
+        else:
+            raise AssertionError("the voided payload never completed")
+        assert msg.value == 9 and crc.value == want
+        st = _lib.CMsgrStats()
+        L.crc32c_msgr_get_stats(ctypes.byref(st))
+        assert st.rx_verified == st0.rx_verified + 1 and st.rx_bad == st0.rx_bad, (st0.rx_verified, st.rx_verified)
+        assert ac.stats()["faults"] >= 1
+    finally:
+        L.crc32c_msgr_conn_destroy(conn)
+        L.crc32c_msgr_set_host_max(prev)
+        ac.close()
 
 
 def sc_context_after_failure_is_replaceable():
