@@ -2,7 +2,7 @@
 """bench.py -- CRC32C GiB/s on device-resident object buffers (BASELINE.json).
 
 One "step" = one pass of the hot path (libpech_crc32c.so's kernels: one
-flat launch for batches of up to 256 buffers, plan + main beyond) over one
+flat launch for batches of up to 4,096 buffers, plan + main beyond) over one
 batch of device-resident synthetic buffers.
 Default workload = BASELINE config 3 / per-GPU shard of config 5:
 256 x 4 MiB buffers (1 GiB) per GPU, rotating between 2 distinct batches
@@ -170,7 +170,7 @@ def main():
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     maxs = max(1, args.streams)
     small_api = args.api == "small" or (args.api == "auto" and int(sizes.max()) < (32 << 10))
-    flat = not small_api and args.op == "crc" and n <= min(args.flat_max, 256)
+    flat = not small_api and args.op == "crc" and n <= min(args.flat_max, 4096)
 
     class Shard:
         """One device's batches: `rotate` distinct resident batches of random
@@ -345,7 +345,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": ("pech_crc32c_direct_copy" if dsts else "pech_crc32c_direct") if small_api else
-                               "pech_crc32c_flat" if flat else ("pech_crc32c_main_copy" if dsts else "pech_crc32c_main"),
+                               ("pech_crc32c_flat" if n <= 256 else "pech_crc32c_flatg") if flat else
+                               ("pech_crc32c_main_copy" if dsts else "pech_crc32c_main"),
                      "bytes_per_launch": algo_bytes, "avg_launch_us": round(avg_kernel_s * 1e6, 2),
                      "launch_us_p10_p50_p90": [round(float(np.percentile(samples, q)), 2) for q in (10, 50, 90)]
                      if len(samples) else None,
@@ -648,7 +649,7 @@ def msgr_latency(args):
 
 def launch_curve(shard, P, torch):
     """Per-launch cost of the device batch path (the flat kernel for up to
-    256 buffers, plan + main kernels beyond) against launch size, for 4 MiB and 64 KiB buffers: 4 / 32 (the async layer's
+    4,096 buffers, plan + main kernels beyond) against launch size, for 4 MiB and 64 KiB buffers: 4 / 32 (the async layer's
     slot) / 128 / 256 / 1024 MiB per launch, carved from the shard's resident
     batches and cycled over distinct regions of them (2 GiB in all, so the
     256 MB Infinity Cache cannot serve a launch).  main_us: HIP events around
@@ -695,7 +696,7 @@ def launch_curve(shard, P, torch):
                              "step_us": round(step_us, 2), "launches": k}
         res["4MiB" if bsz == 4 << 20 else "64KiB"] = row
     return {"unit": "us per launch; frac = launch bytes / main_us / 8 TB/s", "by_buffer_size_then_MiB": res,
-            "path": "crc32c_dev_batch_ws_async, one stream: the flat kernel for up to 256 buffers (--flat-max), "
+            "path": "crc32c_dev_batch_ws_async, one stream: the flat kernels for up to 4,096 buffers (--flat-max), "
                     "plan + main kernels beyond"}
 
 

@@ -274,14 +274,19 @@ static bool capturing(hipStream_t s)
 	return st != hipStreamCaptureStatusNone;
 }
 
-// Batches of at most g_flat_max buffers run as ONE launch (pech_crc32c_flat:
-// no plan kernel) -- C3's 256 x 4 MiB, the async layer's slots of large
+// Batches of at most g_flat_max buffers run as ONE launch (pech_crc32c_flat
+// up to 256 buffers, pech_crc32c_flatg above: no plan kernel) -- C3's 256 x 4 MiB, the async layer's slots of large
 // payloads, a single large message.  Its workgroup 0 publishes the zeroed
 // out[] through the first 8 bytes of the workspace and a tag that must differ
 // from every earlier launch's on that workspace: a process-wide 64-bit
 // counter from a per-process start, so a tag left in recycled memory by
 // another run does not match either.  A graph replays its captured tag, so
 // captured batches take plan + main.
+// Default PECH_FLAT_MAX (256): pech_crc32c_flatg (up to PECH_FLATG_MAX
+// buffers) is opt-in through crc32c_set_flat_max -- its workgroup-wide
+// prologue costs what the plan launch it saves did, so the one-stream step is
+// no faster (32 MiB of 64 KiB buffers 17.8 -> 19.5 us, 256 MiB 56.6 -> 56.9 us,
+// profiles/r06/flatg.txt), while two streams gain 7 % on C4's 64 KiB class.
 static std::atomic<unsigned int> g_flat_max{PECH_FLAT_MAX};
 
 // rows per wave below which a launch spreads its shares wave-major
@@ -1049,7 +1054,7 @@ unsigned int crc32c_set_cpu_max(unsigned int bytes)
 
 unsigned int crc32c_set_flat_max(unsigned int n)
 {
-	return g_flat_max.exchange(n < PECH_FLAT_MAX ? n : PECH_FLAT_MAX);
+	return g_flat_max.exchange(n < PECH_FLATG_MAX ? n : PECH_FLATG_MAX);
 }
 
 int crc32c_get_stats(struct crc32c_stats *st)

@@ -83,6 +83,9 @@ static_assert(PECH_SPLIT_MIN >= 8u, "every slice of a split step needs a row");
 #define L_XINV (L_DEFER_DONE + 16u) // 512 B: x^(-8k), k < 128
 #define L_POOL (L_XINV + 512u)   // 16 B: the workgroup's next pooled item (uniform batches)
 #define L_BYTES (L_POOL + 16u)
+#define L_SCAN L_BYTES           // 256 B: the large flat prologue's per-wave totals and flags (prologue_flatg)
+#define L_BYTES_G (L_SCAN + 256u) // pech_crc32c_flatg only (the other kernels keep their LDS footprint)
+static_assert(L_BYTES_G <= 160u * 1024u, "flatg LDS budget");
 static_assert(L_BYTES <= 160u * 1024u, "main kernel LDS over 160 KiB");
 
 static_assert(L_POWB - L_TAB4 == 4u * (PECH_C_POWB - PECH_C_TAB4), "LDS/consts layout mismatch");
@@ -644,6 +647,23 @@ __device__ __forceinline__ pech_core flat_core(const uint32_t *lds, uint32_t p)
 	return c;
 }
 
+// Large flat batches (pech_crc32c_flatg, PECH_FLAT_MAX < n <= PECH_FLATG_MAX):
+// no LDS table -- 16 B per position would not fit beside the A_128 tables --
+// so a step's descriptors come from the caller's array itself (`g`: the
+// crc32c_desc array, L2-resident after the prologue read it), by SCALAR loads
+// at wave-uniform positions (lgkmcnt: the ring's vector loads are never
+// drained for them), each turned into the LDS table's {addr, rows, meta}.
+__device__ __forceinline__ pech_core flatg_core(const pech_core *__restrict__ g, uint32_t p)
+{
+	const u32x4 v = ((const u32x4 *)g)[uni(p)]; // {addr lo, addr hi, len, seed}
+	pech_core c;
+	c.addr = ((uint64_t)v.y << 32) | v.x;
+	const uint32_t lb = v.x & (PECH_ROW_BYTES - 1u), len = v.z;
+	c.rows = len ? (uint32_t)(((uint64_t)lb + len + PECH_ROW_BYTES - 1u) >> 7) : 0u;
+	c.meta = p | (c.rows ? c.rows * PECH_ROW_BYTES - lb - len : 0u) << 20; // (T mod 2^32: exact, < 128)
+	return c;
+}
+
 // Step.oz bits of lane g8 for a run that ends its buffer (last): the zl flag
 // and the bytes kb of the lane's last-line piece that are the buffer's
 template <bool FLAT>
@@ -669,7 +689,9 @@ __device__ __forceinline__ uint32_t mp_of(uint32_t ra, uint32_t meta)
 // grid: static shares, whose small-buffer steps lie on a grid of 8 positions.
 // FLAT: the descriptors come from the wave's LDS table (flat_core) for
 // positions < nflat, empty buffers included (skipped here).
-template <bool COPY, bool PRE = false, bool FLAT = false>
+// FLATG: the same from the caller's descriptors (`cores` is then the
+// crc32c_desc array; flatg_core).
+template <bool COPY, bool PRE = false, bool FLAT = false, bool FLATG = false>
 __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
 					  const uint32_t *lds, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
 					  uint32_t g8, uint32_t grp, bool grid, const pech_core &spec = pech_core{},
@@ -711,7 +733,9 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 		}
 		const bool hit = PRE && pos == ppos; // wave-uniform
 		pech_core cd;
-		if (FLAT)
+		if (FLATG)
+			cd = flatg_core(cores, pos);
+		else if (FLAT)
 			cd = flat_core(lds, pos);
 		else if (hit)
 			cd = spec; // lanes 0-7 (group 0) hold cores[pos]; uni() reads lane 0
@@ -776,7 +800,17 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			// workspace memory); such entries are never used.
 			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
 			int64_t mdl = 0;
-			if (FLAT) { // each group its own entry (LDS: no scalar-load selects)
+			if (FLATG) { // scalar loads of the 8 positions, each group taking its own
+#pragma unroll
+				for (uint32_t j = 0; j < 8; ++j) {
+					const pech_core dj = flatg_core(cores, min(pos + j, nflat - 1u));
+					const bool mine = grp == j;
+					vlo = mine ? (uint32_t)dj.addr : vlo;
+					vhi = mine ? (uint32_t)(dj.addr >> 32) : vhi;
+					mrows = mine ? dj.rows : mrows;
+					mmeta = mine ? dj.meta : mmeta;
+				}
+			} else if (FLAT) { // each group its own entry (LDS: no scalar-load selects)
 				const pech_core dj = flat_core(lds, min(pos + grp, nflat - 1u));
 				vlo = (uint32_t)dj.addr;
 				vhi = (uint32_t)(dj.addr >> 32);
@@ -1553,6 +1587,122 @@ __device__ __forceinline__ bool prologue_flat(uint32_t *lds, const u32x4 (&dv)[4
 	return true;
 }
 
+// Large flat batches (pech_crc32c_flatg, n <= PECH_FLATG_MAX = 4,096): thread
+// t of the workgroup holds positions 4t .. 4t+3 (dv, loaded at entry with the
+// tables).  Each wave scans its threads' rows (DPP), writes its lanes'
+// in-wave prefixes (L_FLAT, 4 KiB) and its total, smallest / largest row
+// count and seed flag (L_SCAN); after ONE workgroup barrier every wave knows
+// Rtot, the wave offsets and uniformity, takes its share (wave_share) and
+// finds the position holding its first row: the last thread whose prefix
+// is <= r0 (a count over the 1,024 prefixes, 16 per lane), then that thread's
+// 4 descriptors by scalar loads.  No per-position table: steps read the
+// descriptors themselves (flatg_core).  Nothing here is written by the
+// tables' fill, so no second barrier.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+#pragma unroll
+	for (uint32_t d = 1; d < 64u; d <<= 1)
+		v = min(v, (uint32_t)__shfl_xor((int)v, (int)d));
+	return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+	for (uint32_t d = 1; d < 64u; d <<= 1)
+		v = max(v, (uint32_t)__shfl_xor((int)v, (int)d));
+	return v;
+}
+
+__device__ __forceinline__ bool prologue_flatg(uint32_t *lds, const u32x4 (&dv)[4], const pech_desc *__restrict__ descs,
+					       uint32_t n, uint32_t tid, uint32_t lane, uint32_t wave, uint32_t W,
+					       uint32_t rpw_min, Start &st, uint32_t &Rtot, bool &seeds)
+{
+	static_assert(PECH_FLATG_MAX == 4u * PECH_MAIN_THREADS, "flatg: 4 positions per thread of the workgroup");
+	uint32_t rows[4], tsum = 0, rmin = 0xFFFFFFFFu, rmax = 0;
+	bool sd = false;
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k) {
+		const uint32_t p = 4u * tid + k, lb = dv[k].x & (PECH_ROW_BYTES - 1u), len = dv[k].z;
+		rows[k] = p < n && len ? (uint32_t)(((uint64_t)lb + len + PECH_ROW_BYTES - 1u) >> 7) : 0u;
+		tsum += rows[k];
+		rmin = p < n ? min(rmin, rows[k]) : rmin;
+		rmax = p < n ? max(rmax, rows[k]) : rmax;
+		sd = sd || (p < n && dv[k].w != 0u);
+	}
+	const uint32_t incl = wave_incl_scan(tsum);
+	lds[L_FLAT / 4u + tid] = incl - tsum; // the thread's prefix inside its wave
+	rmin = wave_min_u32(rmin);
+	rmax = wave_max_u32(rmax);
+	const bool wsd = __ballot(sd) != 0ull;
+	if (lane == 63u) {
+		lds[L_SCAN / 4u + wave] = incl;
+		lds[L_SCAN / 4u + 16u + wave] = rmin;
+		lds[L_SCAN / 4u + 32u + wave] = rmax;
+		lds[L_SCAN / 4u + 48u + wave] = wsd;
+	}
+	__syncthreads();
+	STAMP(t_scan);
+#ifdef PECH_STAMPS
+	st.t_scan = t_scan;
+#endif
+	// every lane reads the 16 waves' words (broadcast LDS reads)
+	uint32_t tot = 0, woff = 0, umin = 0xFFFFFFFFu, umax = 0, anysd = 0;
+	const uint32_t lw = lane >> 2; // the wave of threads 16 lane .. 16 lane + 15
+#pragma unroll
+	for (uint32_t w = 0; w < PECH_MAIN_WAVES; ++w) {
+		const uint32_t t = lds[L_SCAN / 4u + w];
+		woff += w < lw ? t : 0u;
+		tot += t;
+		umin = min(umin, lds[L_SCAN / 4u + 16u + w]);
+		umax = max(umax, lds[L_SCAN / 4u + 32u + w]);
+		anysd |= lds[L_SCAN / 4u + 48u + w];
+	}
+	Rtot = uni(tot);
+	seeds = uni(anysd) != 0u;
+	const uint32_t U0 = uni(umin);
+	const bool uniform = U0 != 0u && U0 == uni(umax);
+	if (!wave_share<false>(Rtot, W, rpw_min, wave, uniform, false, st))
+		return false; // whole workgroup idle (small batch)
+	st.U0 = U0;
+	st.p0 = st.lr0 = 0;
+	st.jj = st.pjj = st.nzjj = st.nsjj = 0;
+	if (st.rem_all) {
+		const uint32_t r0 = st.r0;
+		// threads whose prefix is <= r0: the last of them holds r0 (a thread
+		// with no rows before it shares the next one's prefix, which is > r0)
+		uint32_t cnt = 0;
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) {
+			const u32x4 v = *(const u32x4 *)(lds + L_FLAT / 4u + 16u * lane + 4u * q);
+			cnt += (woff + v.x <= r0) + (woff + v.y <= r0) + (woff + v.z <= r0) + (woff + v.w <= r0);
+		}
+		const uint32_t ts = lane_value(wave_incl_scan(cnt), 63) - 1u;
+		uint32_t acc = lds[L_FLAT / 4u + ts];
+		for (uint32_t w = 0; w < (ts >> 6); ++w)
+			acc += lds[L_SCAN / 4u + w];
+		acc = uni(acc);
+		uint32_t p0 = 4u * ts, lr0 = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) { // scalar loads: the thread's four descriptors
+			const uint32_t p = 4u * ts + k;
+			const u32x4 d = ((const u32x4 *)descs)[uni(min(p, n - 1u))];
+			const uint32_t lb = d.x & (PECH_ROW_BYTES - 1u);
+			const uint32_t r = p < n && d.z ? (uint32_t)(((uint64_t)lb + d.z + PECH_ROW_BYTES - 1u) >> 7) : 0u;
+			const bool h = r != 0u && acc <= r0 && r0 - acc < r;
+			p0 = h ? p : p0;
+			lr0 = h ? r0 - acc : lr0;
+			acc += r;
+		}
+		st.p0 = uni(p0);
+		st.lr0 = uni(lr0);
+#ifdef PECH_DEBUG_BOUNDS
+		if (lane == 0 && (st.p0 >= n || ts >= PECH_MAIN_THREADS))
+			printf("PECH OOB flatg prologue blk %u wave %u r0 %u p0 %u ts %u n %u\n", blockIdx.x, wave, r0, st.p0, ts, n);
+#endif
+	}
+	return true;
+}
+
 // FLAT (pech_crc32c_flat): the same walk for n <= PECH_FLAT_MAX buffers with
 // no plan kernel -- the descriptors are read at entry (descs) and kept in LDS
 // (prologue_flat), and out[] is zeroed inside the launch, published through
@@ -1604,42 +1754,50 @@ __device__ __forceinline__ void flat_fault(uint64_t *flag, uint64_t *hstat, uint
 #endif
 }
 
-// Flat batches: the seed terms x^(8 len) s of R(s, D) = x^(8|D|) s ^ R(0, D),
-// and the seed itself for an empty buffer, XORed into out[] by the wave that
-// initialises it (the messenger's seeds are 0: nothing to do).
-__device__ __forceinline__ void flat_seeds(const u32x4 (&dv)[4], uint32_t n, uint32_t lane,
-					   const uint32_t *__restrict__ consts, uint32_t *__restrict__ out)
-{
-#pragma unroll
-	for (uint32_t k = 0; k < 4; ++k) {
-		const uint32_t p = 4u * lane + k, len = dv[k].z, seed = dv[k].w;
-		if (p < n && seed != 0u)
-			atomicXor(out + p, len ? shift_bytes(consts + PECH_C_POWB, len, seed) : seed);
-	}
-}
-
 // The claimed job: zeroes (device-scope atomic exchanges: every access to
 // out[] in the launch is a device-scope atomic, ordered at the word itself),
-// the seed terms after them, then FLAT_DONE (a release store).  No acquire on
-// the readers' side: they only XOR, after they read FLAT_DONE.  (An acquire
-// there was an L2 invalidate per wave: +6.5 us per C3 launch.)
-// (The descriptors are read again here, in this rare path, when there are
-// seeds: kept in registers for it, they pushed the kernel past 128 VGPRs.)
+// the seed terms x^(8 len) s of R(s, D) = x^(8|D|) s ^ R(0, D) after them (the
+// seed itself for an empty buffer; the messenger's seeds are 0: nothing to
+// do), then FLAT_DONE (a release store).  No acquire on the readers' side:
+// they only XOR, after they read FLAT_DONE.  (An acquire there was an L2
+// invalidate per wave: +6.5 us per C3 launch.)  (The descriptors are read
+// again here, in this rare path, when there are seeds: kept in registers for
+// it, they pushed the kernel past 128 VGPRs.)  NMAX: the kernel's batch limit
+// (PECH_FLAT_MAX, or PECH_FLATG_MAX for pech_crc32c_flatg).
+template <uint32_t NMAX>
 __device__ __forceinline__ void flat_init(const pech_desc *__restrict__ descs, uint32_t n, uint32_t lane,
 					  const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, uint64_t *flag,
 					  uint64_t tag, bool seeds)
 {
+	if constexpr (NMAX <= PECH_FLAT_MAX) {
 #pragma unroll
-	for (uint32_t k = 0; k < 4; ++k)
-		if (4u * lane + k < n)
-			(void)atomicExch(out + 4u * lane + k, 0u);
+		for (uint32_t k = 0; k < NMAX / 64u; ++k)
+			if (64u * k + lane < n)
+				(void)atomicExch(out + 64u * k + lane, 0u);
+	} else {
+		// flatg: up to 64 words per lane, in a loop over the batch's own words
+		// (unrolled to NMAX, their addresses were hoisted out of the step loop
+		// that calls this and spilled), four exchanges in flight per turn
+		uint32_t *o = out + lane;
+#pragma unroll 1
+		for (uint32_t k = 0; 64u * k < n; k += 4u, o += 256u) {
+#pragma unroll
+			for (uint32_t j = 0; j < 4u; ++j)
+				if (64u * (k + j) + lane < n)
+					(void)atomicExch(o + 64u * j, 0u);
+		}
+	}
 	if (seeds) {
-		u32x4 dv[4];
-#pragma unroll
-		for (uint32_t k = 0; k < 4; ++k)
-			dv[k] = ((const u32x4 *)descs)[min(4u * lane + k, n - 1u)];
 		__threadfence(); // the zeroes are performed before the seed terms land on the same words
-		flat_seeds(dv, n, lane, consts, out);
+#pragma unroll 1
+		for (uint32_t k = 0; k < NMAX / 64u; ++k) {
+			const uint32_t p = 64u * k + lane;
+			if (p >= n)
+				break;
+			const u32x4 d = ((const u32x4 *)descs)[p];
+			if (d.w != 0u)
+				atomicXor(out + p, d.z ? shift_bytes(consts + PECH_C_POWB, d.z, d.w) : d.w);
+		}
 	}
 	if (lane == 0) {
 		(void)atomicExch((uint32_t *)(flag + 1), 0u); // the publication count (flat_publish)
@@ -1659,6 +1817,7 @@ __device__ __forceinline__ void flat_init(const pech_desc *__restrict__ descs, u
 // test library's fault hook, 0 from the release library):
 // PECH_FLAT_T_TIMEOUT makes every wave that reaches this wait take the
 // timeout at once.
+template <uint32_t NMAX>
 __device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &ready,
 					   const pech_desc *__restrict__ descs, uint32_t n, uint32_t lane,
 					   const uint32_t *__restrict__ consts, uint32_t *__restrict__ out, bool seeds,
@@ -1676,7 +1835,7 @@ __device__ __forceinline__ void flat_ready(uint64_t *flag, uint64_t tag, bool &r
 			if (lane == 0)
 				got = atomicCAS((unsigned long long *)flag, (unsigned long long)v, (unsigned long long)FLAT_INIT(tag));
 			if (uni64(got) == v) {
-				flat_init(descs, n, lane, consts, out, flag, tag, seeds);
+				flat_init<NMAX>(descs, n, lane, consts, out, flag, tag, seeds);
 				break;
 			}
 			continue; // another wave claimed it first
@@ -1713,6 +1872,7 @@ __device__ __forceinline__ void vm_done()
 // detected event, not stale CRCs.  The host reads hstat
 // after the launch has completed, which orders every store of the kernel.
 // (PECH_FLAT_T_NOPUB, test library only: the publication is skipped.)
+template <uint32_t NMAX>
 __device__ __forceinline__ void flat_publish(uint64_t *flag, uint32_t nlive, uint32_t n, uint32_t lane,
 					     uint32_t *__restrict__ out, uint32_t *__restrict__ hout, uint64_t *hstat,
 					     uint64_t tag, uint32_t test)
@@ -1728,8 +1888,8 @@ __device__ __forceinline__ void flat_publish(uint64_t *flag, uint32_t nlive, uin
 	if (test & PECH_FLAT_T_NOPUB)
 		return;
 	asm volatile("" ::: "memory");
-#pragma unroll
-	for (uint32_t k = 0; k < PECH_FLAT_MAX / 64u; ++k) {
+#pragma unroll(NMAX <= PECH_FLAT_MAX ? NMAX / 64u : 1u)
+	for (uint32_t k = 0; 64u * k < n; ++k) {
 		const uint32_t p = 64u * k + lane;
 		if (p < n)
 			hout[p] = __hip_atomic_load(out + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1743,7 +1903,7 @@ __device__ __forceinline__ void flat_publish(uint64_t *flag, uint32_t nlive, uin
 	}
 }
 
-template <bool COPY, uint32_t U, bool FLAT = false>
+template <bool COPY, uint32_t U, bool FLAT = false, bool FLATG = false>
 __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
 					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
 					  const uint32_t *__restrict__ nzs, uint32_t n,
@@ -1753,7 +1913,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 					  uint64_t *hstat = nullptr, uint32_t test = 0u)
 {
 	static_assert(!(FLAT && COPY), "flat batches: CRC only");
+	static_assert(FLAT || !FLATG, "FLATG is a flat mode");
+	constexpr uint32_t NMAX = FLATG ? PECH_FLATG_MAX : PECH_FLAT_MAX; // flat: the launch's batch limit
 	const uint32_t tid = threadIdx.x;
+	// flat steps read {addr, rows, meta} per position: FLATG from the caller's
+	// descriptors (flatg_core), FLAT from the wave's LDS table
+	const pech_core *const gdesc = FLATG ? (const pech_core *)descs : cores;
 	STAMP(t_entry);
 #ifdef PECH_KARGS_AT_ENTRY
 	// every kernel argument in SGPRs at entry, in one scalar round: on demand,
@@ -1817,7 +1982,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	uint32_t rows0 = 0, pg = 0, cg = 0, lrg = 0;
 	pech_core spec = pech_core{};
 	u32x4 lr4[4], dv[4];
-	if constexpr (FLAT) {
+	if constexpr (FLATG) {
+		// the batch's descriptors, 4 per THREAD of the workgroup (64 contiguous bytes), with the tables
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k)
+			dv[k] = ((const u32x4 *)descs)[min(4u * tid + k, n - 1u)];
+	} else if constexpr (FLAT) {
 		// the batch's descriptors, 4 per lane (64 contiguous bytes), with the tables
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k)
@@ -1912,21 +2082,29 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	bool early_fill, live;
 	if constexpr (FLAT) {
 		uint32_t Rtot;
-		live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot);
-		seeds = __ballot((4u * lane < n && dv[0].w) || (4u * lane + 1u < n && dv[1].w) ||
-				 (4u * lane + 2u < n && dv[2].w) || (4u * lane + 3u < n && dv[3].w)) != 0ull;
+		if constexpr (FLATG) {
+			// the tables go in before the prologue's barrier, which publishes
+			// them with the scan: flatg's only barrier (a fill behind the prime
+			// would take a second one, 1.5 us p50 in 256 MiB launches)
+			fill_tables(false);
+			live = prologue_flatg(lds, dv, descs, n, tid, lane, wave, W, rpw_min, sv, Rtot, seeds);
+		} else {
+			live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot);
+			seeds = __ballot((4u * lane < n && dv[0].w) || (4u * lane + 1u < n && dv[1].w) ||
+					 (4u * lane + 2u < n && dv[2].w) || (4u * lane + 3u < n && dv[3].w)) != 0ull;
+		}
 		if (blockIdx.x == 0 && wave == 0) {
 			// (lane 0's exchange: a claim of this launch already there -- another
 			// wave got in first -- leaves the job to it; a FLAT_DONE it
 			// overwrote goes back)
 			const uint64_t c0 = lane_value((uint32_t)claim0, 0) | (uint64_t)lane_value((uint32_t)(claim0 >> 32), 0) << 32;
 			if ((c0 >> 1) != tag)
-				flat_init(descs, n, lane, consts, out, flag, tag, seeds);
+				flat_init<NMAX>(descs, n, lane, consts, out, flag, tag, seeds);
 			else if (c0 == FLAT_DONE(tag) && lane == 0)
 				__hip_atomic_store(flag, FLAT_DONE(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 		if (hout && Rtot == 0u && blockIdx.x == 0 && wave == 0) // no rows at all: out[] holds the seeds (flat_init above)
-			flat_publish(flag, 0u, n, lane, out, hout, hstat, tag, test);
+			flat_publish<NMAX>(flag, 0u, n, lane, out, hout, hstat, tag, test);
 		if (!live)
 			return; // whole workgroup idle (small batch)
 		// Flat launches fill late at every size: with the wave-major shares of
@@ -1939,7 +2117,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #else
 		early_fill = false;
 #endif
-		if (early_fill) {
+		if (FLATG) {
+			early_fill = true; // (filled and published above)
+		} else if (early_fill) {
 			fill_tables(false);
 			__syncthreads();
 		}
@@ -2003,7 +2183,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	}
 	Step S;
 	if constexpr (FLAT)
-		S = plan_step<false, false, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false, pech_core{}, 0u, n);
+		S = plan_step<false, false, true, FLATG>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false, pech_core{},
+							 0u, n);
 	else
 		S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
 		       : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
@@ -2189,6 +2370,16 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// already fetch the next step's first rows
 		const uint32_t r = blk * U;
 		ring[U - 1] = LD_PIECE(S, row_addr(S.ad, min(r + U - 1, last), STEP_ZOFF(S), rsb), 4);
+		// Flat: the out[] flag again, looked at when this step's run is
+		// XORed (after the block): the early read at the prime came before
+		// the claiming wave had zeroed out[] in most waves, and polling then
+		// cost every wave a round trip at its first XOR (~1-2 us of busy time
+		// in 256 MiB launches of 64 KiB buffers, profiles/r06/stamps_flatg.txt).
+		// Unconditional, as one more load in the ring's count (vmcnt(7) at its
+		// use, no drain).
+		uint64_t seen_l = 0;
+		if constexpr (FLAT)
+			seen_l = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef PECH_STAMP_FIN // stamps build: time spent planning steps inside the loop (sum, 25 % stamp slot)
 		const uint64_t t_pl0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2220,8 +2411,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			}
 		}
 #ifndef PECH_NO_NEXT_SPEC
-		const Step N = FLAT ? plan_step<false, false, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, false,
-								    pech_core{}, 0u, n)
+		const Step N = FLAT ? plan_step<false, false, true, FLATG>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
+									   false, pech_core{}, 0u, n)
 			   : il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 			   : COPY ? plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid)
 				  : plan_step<COPY, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid, nspec, nppos);
@@ -2240,8 +2431,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			nspec = load_spec(cores, nppos + grp);
 		}
 #else // A/B: N's descriptors loaded when N is planned
-		const Step N = FLAT ? plan_step<false, false, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, false,
-								    pech_core{}, 0u, n)
+		const Step N = FLAT ? plan_step<false, false, true, FLATG>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
+									   false, pech_core{}, 0u, n)
 			   : il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 				  : plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
 #endif
@@ -2292,8 +2483,10 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifdef PECH_STAMP_FIN // stamps build: the last step's fold + shift (75 % stamp -> its start)
 		tq[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-		if (FLAT)
-			flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds, hstat, test);
+		if constexpr (FLAT) {
+			ready = ready || (uni64(seen_l) == FLAT_DONE(tag) && !(test & PECH_FLAT_T_TIMEOUT));
+			flat_ready<NMAX>(flag, tag, ready, descs, n, lane, consts, out, seeds, hstat, test);
+		}
 		finish_run<!COPY>(lds, g8, s0, s1, s2, s3, step_m<FLAT>(S), STEP_RA(S), tpow, S.nu != 0, out, step_orig<FLAT>(S));
 		tpow = tpow_n;
 #ifdef PECH_STAMP_FIN
@@ -2320,7 +2513,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		static_assert(PECH_DEFER_SLOTS == 64u, "one slot per lane of the flushing wave");
 		if (done == PECH_MAIN_WAVES - 1u) {
 			if (FLAT)
-				flat_ready(flag, tag, ready, descs, n, lane, consts, out, seeds, hstat, test);
+				flat_ready<NMAX>(flag, tag, ready, descs, n, lane, consts, out, seeds, hstat, test);
 			const uint32_t k = lds[L_DEFER / 4u + lane];
 			bool flush = k != PECH_DEFER_EMPTY;
 #ifdef PECH_DEBUG_BOUNDS
@@ -2335,7 +2528,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #endif
 				atomicXor(out + k, lds[L_DEFER / 4u + PECH_DEFER_SLOTS + lane]);
 			if (FLAT && hout)
-				flat_publish(flag, sv.nlive, n, lane, out, hout, hstat, tag, test);
+				flat_publish<NMAX>(flag, sv.nlive, n, lane, out, hout, hstat, tag, test);
 		}
 	}
 #ifdef PECH_STAMPS
@@ -2395,6 +2588,22 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_f
 	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
 	main_body<false, PECH_U, true>(lds, nullptr, nullptr, nullptr, nullptr, n, consts, out, rpw_min, nullptr, descs, flag,
 				       tag, hout, hstat, test);
+}
+
+// The same for PECH_FLAT_MAX < n <= PECH_FLATG_MAX buffers (the messenger's
+// slots of 64 KiB payloads, 512 to a 32 MiB slot; C4's 64 KiB class, 4,096
+// per 256 MiB launch): one launch instead of plan + main.  Its prologue
+// scans the rows over the whole workgroup (prologue_flatg) and its steps read
+// the descriptors in place (flatg_core); out[] is initialised and published
+// as in pech_crc32c_flat.
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_flatg(
+	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	uint32_t rpw_min, uint64_t *__restrict__ flag, uint64_t tag, uint32_t *__restrict__ hout, uint64_t *hstat,
+	uint32_t test)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES_G / 4u];
+	main_body<false, PECH_U, true, true>(lds, nullptr, nullptr, nullptr, nullptr, n, consts, out, rpw_min, nullptr, descs,
+					     flag, tag, hout, hstat, test);
 }
 
 // ---- direct kernel: small-buffer batches without a plan kernel -------------
@@ -2826,10 +3035,14 @@ extern "C" hipError_t pech_launch_flat(const pech_desc *descs, uint32_t n, const
 				       uint32_t ncu, uint32_t rpw_min, uint64_t *flag, uint64_t tag, hipStream_t stream,
 				       hipEvent_t ev_start, hipEvent_t ev_stop, uint32_t *hout, uint64_t *hstat, uint32_t test)
 {
-	if (n == 0 || n > PECH_FLAT_MAX || ((uintptr_t)flag & 7u))
+	if (n == 0 || n > PECH_FLATG_MAX || ((uintptr_t)flag & 7u))
 		return hipErrorInvalidValue;
-	hipExtLaunchKernelGGL(pech_crc32c_flat, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u, descs,
-			      n, consts, out, rpw_min, flag, tag, hout, hstat, test);
+	if (n <= PECH_FLAT_MAX)
+		hipExtLaunchKernelGGL(pech_crc32c_flat, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u,
+				      descs, n, consts, out, rpw_min, flag, tag, hout, hstat, test);
+	else
+		hipExtLaunchKernelGGL(pech_crc32c_flatg, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u,
+				      descs, n, consts, out, rpw_min, flag, tag, hout, hstat, test);
 	return hipGetLastError();
 }
 
@@ -2852,6 +3065,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.33 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.33 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) ",flatg<=" PECH_STR(PECH_FLATG_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -73,6 +73,7 @@
 #ifndef PECH_FLAT_MAX
 #define PECH_FLAT_MAX 256u        /* device batches of up to this many buffers: one launch, no plan kernel */
 #endif
+#define PECH_FLATG_MAX 4096u      /* ... and up to this many: one launch of pech_crc32c_flatg (descriptors read in place) */
 #define PECH_SMALL_MAX 65536u     /* drop-in crc32c(): one-launch path up to this */
 #define PECH_DROPIN_CPU_MAX_DEFAULT (4u << 20) /* drop-in crc32c(): host routine up to this */
 /* payload of one launch: rows (128 B) are counted in 32 bits, so < 512 GiB */

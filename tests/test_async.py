@@ -177,11 +177,13 @@ def test_async_context_per_device(monkeypatch):
 def test_async_results_stored_by_the_kernel(monkeypatch, host_out):
     """Flat and direct launches store a slot's results in its pinned host
     array themselves (no copy after the kernel; PECH_ASYNC_HOST_OUT=0 keeps
-    the copy, as planned batches of more than 256 pieces always do), and a
+    the copy, as planned batches of more than 4,096 pieces always do), and a
     lone small batch is polled by the context's thread.  Lone payloads one at
     a time: 64 KiB and 1 MiB (flat), 4 KiB and 20 KiB pieces (direct), with
-    and without seeds, a zero-length one; then one slot of 300 x 40 KiB
-    (plan + main)."""
+    and without seeds, a zero-length one; then slots of 300 x 40 KiB
+    (plan + main at the default flat limit; pech_crc32c_flatg, stored by the
+    kernel, at 4,096), then one of 4,200 pieces, one
+    of them 40 KiB (plan + main, results copied)."""
     import pech_amd as P
 
     monkeypatch.setenv("PECH_ASYNC_HOST_OUT", host_out)
@@ -205,18 +207,40 @@ def test_async_results_stored_by_the_kernel(monkeypatch, host_out):
     assert lone >= 3 * (len(sizes) - 1), st
     assert st["polled"] == lone, st  # every lone batch of <= 8 MiB polled
     assert st["host_out"] == (lone if host_out == "1" else 0), st
-    # more than 256 pieces in one slot: plan + main, results copied
+    # 300 pieces in one slot: plan + main at the default flat limit (256),
+    # pech_crc32c_flatg with results stored by the kernel at 4,096
     base = dict(got)
-    for i in range(300):
-        b = rng.integers(0, 256, 40000, dtype=np.uint8)
+    prev = P.set_flat_max(256)
+    try:
+        for fm, stored in ((256, 0), (4096, 1 if host_out == "1" else 0)):
+            P.set_flat_max(fm)
+            st1 = ac.stats()
+            for i in range(300):
+                b = rng.integers(0, 256, 40000, dtype=np.uint8)
+                keep.append(b)
+                want[k] = O.crc(i, b)
+                ac.submit(b.ctypes.data, b.size, i, lambda crc, err, k=k: got.__setitem__(k, (crc, err)), keep=b)
+                k += 1
+            ac.drain()
+            assert got == {i: (want[i], 0) for i in range(k)}
+            st2 = ac.stats()
+            assert st2["launches"] == st1["launches"] + 1, (st1, st2)
+            assert st2["host_out"] - st1["host_out"] == stored, (fm, st1, st2)
+    finally:
+        P.set_flat_max(prev)
+    # more than 4,096 pieces in one slot: plan + main, results copied
+    P.set_flat_max(4096)
+    for i in range(4200):
+        b = rng.integers(0, 256, 40000 if i == 77 else 4096, dtype=np.uint8)
         keep.append(b)
         want[k] = O.crc(i, b)
         ac.submit(b.ctypes.data, b.size, i, lambda crc, err, k=k: got.__setitem__(k, (crc, err)), keep=b)
         k += 1
     ac.drain()
     assert got == {i: (want[i], 0) for i in range(k)}
-    st2 = ac.stats()
-    assert st2["launches"] > lone and st2["host_out"] - st["host_out"] < st2["launches"] - lone, (st, st2)
+    st3 = ac.stats()
+    P.set_flat_max(prev)
+    assert st3["launches"] == st2["launches"] + 1 and st3["host_out"] == st2["host_out"], (st2, st3)
     assert base.items() <= got.items()
     ac.close()
 

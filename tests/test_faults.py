@@ -343,7 +343,6 @@ def sc_flat_timeout_dropin_recomputed_on_host():
 def sc_flat_timeout_batch_fails_loudly():
     import oracle_lib as O
     import pech_amd as P
-    import torch
 
     rng = np.random.default_rng(52)
     bufs = _big_payloads(rng, 5)
@@ -357,21 +356,41 @@ def sc_flat_timeout_batch_fails_loudly():
     except P.Crc32cError:
         pass
     assert P.crc32c_batch([b.tobytes() for b in bufs]) == want  # the next call is exact
-    # a device entry point's caller reads the fault from the counters
-    dev = torch.device("cuda", 0)
-    t = [torch.from_numpy(b).to(dev) for b in bufs]
-    descs = P.make_descs([x.data_ptr() for x in t], [x.numel() for x in t], device=dev)
-    out = torch.zeros(len(t), dtype=torch.int32, device=dev)
-    ws = torch.empty(P.workspace_bytes(len(t)), dtype=torch.uint8, device=dev)
-    inject(SITE_FLAT_TIMEOUT, 1)
-    P.dev_batch_ws_async(descs, out, ws)
-    torch.cuda.synchronize()
-    mid = P.stats()
-    assert mid["gpu_faults"] == before["gpu_faults"] + 2, (before, mid)
-    P.dev_batch_ws_async(descs, out, ws)
-    torch.cuda.synchronize()
-    assert out.cpu().numpy().view(np.uint32).tolist() == want
-    assert P.stats()["gpu_faults"] == mid["gpu_faults"]
+    # a device entry point's caller reads the fault from the counters (device
+    # memory from the library's own HIP runtime: this child process has
+    # initialised it before torch could)
+    from pech_amd import _lib
+    L = _lib.lib()
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    total = sum(b.size for b in bufs)
+    dbuf, ddesc, dout, dws = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    wsb = L.crc32c_dev_workspace_bytes(len(bufs))
+    for p, nb in ((dbuf, total), (ddesc, 16 * len(bufs)), (dout, 4 * len(bufs)), (dws, wsb)):
+        assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(nb)) == 0
+    try:
+        descs = np.zeros(len(bufs), dtype=[("addr", "<u8"), ("len", "<u4"), ("seed", "<u4")])
+        off = 0
+        for i, b in enumerate(bufs):
+            assert hip.hipMemcpy(ctypes.c_void_p(dbuf.value + off), b.ctypes.data_as(ctypes.c_void_p),
+                                 ctypes.c_size_t(b.size), 1) == 0
+            descs[i] = (dbuf.value + off, b.size, 0)
+            off += b.size
+        assert hip.hipMemcpy(ddesc, descs.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(descs.nbytes), 1) == 0
+        res = np.zeros(len(bufs), dtype=np.uint32)
+        for armed in (True, False):
+            if armed:
+                inject(SITE_FLAT_TIMEOUT, 1)
+            assert L.crc32c_dev_batch_ws_async(ddesc, dout, len(bufs), dws, wsb, None) == 0
+            assert hip.hipDeviceSynchronize() == 0
+            if armed:
+                mid = P.stats()
+                assert mid["gpu_faults"] == before["gpu_faults"] + 2, (before, mid)
+        assert hip.hipMemcpy(res.ctypes.data_as(ctypes.c_void_p), dout, ctypes.c_size_t(res.nbytes), 2) == 0
+        assert res.tolist() == want
+        assert P.stats()["gpu_faults"] == mid["gpu_faults"]
+    finally:
+        for p in (dbuf, ddesc, dout, dws):
+            hip.hipFree(p)
 
 
 def sc_flat_timeout_async_slot_fails_not_sticky():

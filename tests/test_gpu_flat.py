@@ -1,14 +1,16 @@
 """GPU parity of the one-launch device batch (pech_crc32c_flat: batches of at
-most 256 buffers with no plan kernel, crc32c_set_flat_max) against the
-oracle, bit-exact, and against the two-launch plan + main path on the same
-batch.  Cases particular to this kernel: its rows cover ALL of a buffer's
+most 256 buffers with no plan kernel; pech_crc32c_flatg: up to 4,096, its
+prologue scanning over the workgroup and its steps reading the descriptors
+in place; crc32c_set_flat_max) against the oracle, bit-exact, and against
+the two-launch plan + main path on the same batch.  Cases particular to this kernel: its rows cover ALL of a buffer's
 bytes (last-line pieces kept below kb bytes, x^(-8T) at the end), empty
 buffers kept in place in descriptor order (runs of them before large ones),
 seeds added by the wave that initialises out[], out[] zeroed in the launch
 and published by a per-launch tag (garbage in out[], back-to-back launches
 on one workspace, two and four streams at once, whose workgroups interleave
 on the CUs), the uniform pool, one buffer split over many workgroups, and
-the 256 / 257 boundary to the planned path."""
+the 256 / 257 boundary between the two flat kernels and 4,096 / 4,097 to the
+planned path."""
 import numpy as np
 import pytest
 
@@ -16,7 +18,7 @@ import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
 
-FLAT_MAX = 256
+FLAT_MAX = 4096  # PECH_FLATG_MAX: pech_crc32c_flat up to 256 buffers, pech_crc32c_flatg above
 
 
 @pytest.fixture(scope="module")
@@ -85,12 +87,14 @@ def test_known_answer(torch_dev, P, route):
     assert got[2] == 0x1234
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 63, 64, 65, 255, 256, 257])
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 63, 64, 65, 255, 256, 257, 300, 511, 512, 1023, 1024, 1025, 2049, 4095,
+                               4096, 4097])
 def test_random_sizes(torch_dev, P, route, n):
-    # sizes from 0 to 5 MiB at random byte offsets, random seeds, empties
+    # sizes from 0 to 5 MiB (at most ~2 GiB a batch) at random byte offsets,
+    # random seeds, empties
     torch, dev = torch_dev
     rng = np.random.default_rng(1000 + n)
-    lens = rng.integers(0, 5 << 20, n)
+    lens = rng.integers(0, min(5 << 20, (2 << 30) // n), n)
     lens[rng.random(n) < 0.15] = 0
     small = rng.random(n) < 0.3
     lens[small] = rng.integers(1, 300, int(small.sum()))
@@ -101,38 +105,43 @@ def test_random_sizes(torch_dev, P, route, n):
     check(torch, P, buf, offs, lens, seeds)
 
 
+@pytest.mark.parametrize("copies", [1, 8])
 @pytest.mark.parametrize("L", [1, 15, 16, 17, 113, 127, 128, 129, 255, 4096, 4100, 65537])
-def test_last_line_masks(torch_dev, P, route, L):
+def test_last_line_masks(torch_dev, P, route, L, copies):
     # every start offset within a line: head and tail in one line (small L),
-    # T from 0 to 127, a buffer ending exactly on a line (T = 0)
+    # T from 0 to 127, a buffer ending exactly on a line (T = 0); 8 copies:
+    # 1,024 buffers (pech_crc32c_flatg)
     torch, dev = torch_dev
-    offs = np.arange(128, dtype=np.int64) * (L + 128 + 37) + np.arange(128)
+    m = 128 * copies
+    offs = np.arange(m, dtype=np.int64) * (L + 128 + 37) + np.arange(m) % 128
     buf = rand_buf(torch, dev, int(offs[-1]) + L + 64, L)
-    check(torch, P, buf, offs, [L] * 128)
+    check(torch, P, buf, offs, [L] * m)
 
 
-def test_empty_runs_before_large_buffers(torch_dev, P, route):
+@pytest.mark.parametrize("cap", [256, 3000])
+def test_empty_runs_before_large_buffers(torch_dev, P, route, cap):
     # runs of 8 and more empty buffers (no rows: skipped in place) between
-    # large ones, and a batch that ends in empties
+    # large ones, and a batch that ends in empties; whole workgroup-scan
+    # threads (4 positions each) without rows in the large batch
     torch, dev = torch_dev
     rng = np.random.default_rng(5)
     lens = []
-    for k in range(12):
-        lens += [0] * int(rng.integers(1, 20))
-        lens += [int(rng.integers(100000, 3 << 20))]
-    lens += [0] * 9
-    lens = np.asarray(lens[:FLAT_MAX])
+    while len(lens) < cap - 9:
+        lens += [0] * int(rng.integers(1, 20 if cap <= 256 else 60))
+        lens += [int(rng.integers(100000, 3 << 20 if cap <= 256 else 1 << 20))]
+    lens = np.asarray(lens[:cap - 9] + [0] * 9)
     seeds = rng.integers(0, 1 << 32, len(lens), dtype=np.uint64)
     offs, total = layout(lens, rng)
     buf = rand_buf(torch, dev, total, 5)
     check(torch, P, buf, offs, lens, seeds)
 
 
-def test_all_empty(torch_dev, P, route):
+@pytest.mark.parametrize("n", [40, 2000])
+def test_all_empty(torch_dev, P, route, n):
     torch, dev = torch_dev
     buf = rand_buf(torch, dev, 64, 1)
-    got = dev_crcs(torch, P, buf, [0] * 40, [0] * 40, list(range(40)))
-    assert [int(x) for x in got] == list(range(40))
+    got = dev_crcs(torch, P, buf, [0] * n, [0] * n, list(range(n)))
+    assert [int(x) for x in got] == list(range(n))
 
 
 @pytest.mark.parametrize("L,off", [((64 << 20) + 12345, 3), (33 << 20, 0), (4 << 20, 0), (300 * 128 + 5, 77)])
@@ -147,7 +156,8 @@ def test_one_buffer_over_many_workgroups(torch_dev, P, route, L, off):
         assert int(got[0]) == O.crc(seed, host[off:off + L])
 
 
-@pytest.mark.parametrize("n,L,gap", [(256, 4 << 20, 0), (200, (1 << 20) + 3, 5), (256, 65536, 0), (16, 16 << 20, 128)])
+@pytest.mark.parametrize("n,L,gap", [(256, 4 << 20, 0), (200, (1 << 20) + 3, 5), (256, 65536, 0), (16, 16 << 20, 128),
+                                     (4096, 65536, 0), (1024, 1 << 20, 0), (600, (1 << 20) + 3, 5), (300, 4 << 20, 0)])
 def test_uniform_pool(torch_dev, P, route, n, L, gap):
     # every buffer the same rows: the workgroup pool (positions by division)
     torch, dev = torch_dev
@@ -166,8 +176,8 @@ def test_back_to_back_launches_one_workspace(torch_dev, P):
     rng = np.random.default_rng(77)
     bufs, outs = [], []
     for k in range(40):
-        n = int(rng.integers(1, FLAT_MAX + 1))
-        lens = rng.integers(0, 1 << 20, n)
+        n = int(rng.integers(1, 300)) if k % 2 else int(rng.integers(1, FLAT_MAX + 1))
+        lens = rng.integers(0, min(1 << 20, (512 << 20) // n), n)
         offs, total = layout(lens, rng, 64)
         buf = rand_buf(torch, dev, total, 100 + k)
         out, descs = dev_crcs(torch, P, buf, offs, lens, ws=ws, sync=False)
@@ -197,10 +207,11 @@ def test_two_streams_two_workspaces(torch_dev, P):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), O.crcs(buf.cpu().numpy(), offs, lens))
 
 
-def test_flat_and_planned_agree_on_c3(torch_dev, P):
-    # BASELINE C3 (256 x 4 MiB) through both paths, every output vs the oracle
+@pytest.mark.parametrize("n,L", [(256, 4 << 20), (4096, 64 << 10)])
+def test_flat_and_planned_agree_on_c3(torch_dev, P, n, L):
+    # BASELINE C3 (256 x 4 MiB) and C4's 64 KiB class (4,096 x 64 KiB) through
+    # both paths, every output vs the oracle
     torch, dev = torch_dev
-    n, L = 256, 4 << 20
     buf = rand_buf(torch, dev, n * L, 33)
     offs = np.arange(n, dtype=np.int64) * L
     want = O.crcs(buf.cpu().numpy(), offs, [L] * n)
@@ -219,7 +230,8 @@ def test_set_flat_max_clamps(P):
     assert P.set_flat_max(prev) == FLAT_MAX
 
 
-def test_concurrent_flat_launches_on_four_streams(torch_dev, P):
+@pytest.mark.parametrize("n,L", [(128, 1 << 20), (1024, 256 << 10)])
+def test_concurrent_flat_launches_on_four_streams(torch_dev, P, n, L):
     """Flat launches on four streams at once, each large enough to fill the
     chip: their workgroups interleave on the CUs, so one launch's workgroup 0
     may wait for a CU while its other workgroups reach their first XOR.
@@ -230,7 +242,6 @@ def test_concurrent_flat_launches_on_four_streams(torch_dev, P):
     streams = [torch.cuda.Stream(device=dev) for _ in range(4)]
     wss = [torch.empty(P.workspace_bytes(FLAT_MAX), dtype=torch.uint8, device=dev) for _ in range(8)]
     rng = np.random.default_rng(44)
-    n, L = 128, 1 << 20
     bufs = [rand_buf(torch, dev, n * L + 64, 500 + k) for k in range(4)]
     torch.cuda.synchronize()
     jobs = []
@@ -246,3 +257,16 @@ def test_concurrent_flat_launches_on_four_streams(torch_dev, P):
     for k, (b, off, lens, seeds, out, _) in enumerate(jobs):
         want = O.crcs(hosts[k % 4], off, lens, seeds)
         assert np.array_equal(out.cpu().numpy().view(np.uint32), want), k
+
+
+def test_one_huge_buffer_among_many(torch_dev, P, route):
+    # pech_crc32c_flatg with one 64 MiB buffer among 700 small ones: shares of
+    # many waves inside one position, the workgroup scan's thread holding it
+    torch, dev = torch_dev
+    rng = np.random.default_rng(9)
+    lens = rng.integers(0, 40000, 701)
+    lens[350] = (64 << 20) + 999
+    seeds = rng.integers(0, 1 << 32, 701, dtype=np.uint64)
+    offs, total = layout(lens, rng)
+    buf = rand_buf(torch, dev, total, 9)
+    check(torch, P, buf, offs, lens, seeds)
