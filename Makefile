@@ -16,7 +16,7 @@ OBJ = build/crc32c_kernels.o $(HOST_OBJ)
 REF_PRESENT := $(wildcard /root/reference/src/ceph/messenger.c)
 
 all: $(LIB) oracle build/msgr_sim build/msgr_conn_sim build/dropin_kat build/coro_stack build/dropin_bench build/launch_cost \
-     build/lib_dbg.so build/lib_test.so build/hbm_probe build/sched_probe $(if $(REF_PRESENT),build/msgr_loopback)
+     build/lib_dbg.so build/lib_test.so build/hbm_probe build/sched_probe build/host_probe $(if $(REF_PRESENT),build/msgr_loopback)
 
 build/crc32c_kernels.o: pech_amd/csrc/crc32c_kernels.hip $(HDR)
 	@mkdir -p build
@@ -140,5 +140,9 @@ build/hbm_probe: tools/hbm_probe.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@
 
 build/sched_probe: tools/sched_probe.hip
+	@mkdir -p build
+	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@
+
+build/host_probe: tools/host_probe.hip
 	@mkdir -p build
 	$(HIPCC) -O3 --offload-arch=$(ARCH) $< -o $@

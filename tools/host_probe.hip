@@ -1,0 +1,142 @@
+// host_probe.hip -- GPU-box probe (not product code): how fast a kernel reads
+// PINNED HOST memory over the host link, against the copy engines, for the
+// messenger's zero-copy slots (the zero-copy kernel reads
+// 4 MiB payloads at ~37.6 GiB/s where the SDMA engines move 52 GiB/s).
+//
+//   host_probe <MiB per launch> <reps>
+//
+// Shapes (each: one launch over the buffer, the sum of its words to keep the
+// loads; GB/s over the best of <reps>):
+//   rows-nt      the CRC kernel's access: 8-lane groups, 16 B per lane per
+//                128-byte row, 8 rows in flight per lane, nontemporal,
+//                one 1024-thread workgroup per CU, static contiguous slices
+//   rows         the same without the nontemporal hint
+//   grid-nt/grid one 16-byte element per thread, a grid over the whole buffer
+//   grid-x1      one 4-byte element per thread
+//   sdma         hipMemcpyAsync host -> device of the same buffer
+// The buffer is hipHostMalloc'd (default flags: coarse-grained pinned), as the
+// library's crc32c_pages memory is, and also hipHostMallocCoherent (fine-grained).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define CHECK(x)                                                                                  \
+	do {                                                                                      \
+		hipError_t e_ = (x);                                                              \
+		if (e_ != hipSuccess) {                                                           \
+			fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+			exit(1);                                                                  \
+		}                                                                                 \
+	} while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__global__ __launch_bounds__(1024) void rows_kernel(const u32x4 *p, uint64_t nrows, uint32_t *sink)
+{
+	// rows are 128 B = 8 x 16 B; group g of the workgroup's 128 groups walks a
+	// contiguous slice of the rows, 8 in flight per lane
+	const uint32_t tid = threadIdx.x, g8 = tid & 7u;
+	const uint64_t grp = (uint64_t)blockIdx.x * 128u + (tid >> 3), ngrp = (uint64_t)gridDim.x * 128u;
+	const uint64_t r0 = nrows * grp / ngrp, r1 = nrows * (grp + 1u) / ngrp;
+	u32x4 acc = (u32x4)(0u);
+	uint64_t r = r0;
+	for (; r + 8u <= r1; r += 8u) {
+		u32x4 v[8];
+#pragma unroll
+		for (uint32_t i = 0; i < 8u; ++i)
+			v[i] = NT ? __builtin_nontemporal_load(p + (r + i) * 8u + g8) : p[(r + i) * 8u + g8];
+#pragma unroll
+		for (uint32_t i = 0; i < 8u; ++i)
+			acc ^= v[i];
+	}
+	for (; r < r1; ++r)
+		acc ^= NT ? __builtin_nontemporal_load(p + r * 8u + g8) : p[r * 8u + g8];
+	if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u)
+		sink[0] = 1u;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void grid_kernel(const u32x4 *p, uint64_t n, uint32_t *sink)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) {
+		const u32x4 v = NT ? __builtin_nontemporal_load(p + i) : p[i];
+		if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u)
+			sink[0] = 1u;
+	}
+}
+
+__global__ __launch_bounds__(256) void grid_x1_kernel(const uint32_t *p, uint64_t n, uint32_t *sink)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n && p[i] == 0x9E3779B9u)
+		sink[0] = 1u;
+}
+
+int main(int argc, char **argv)
+{
+	const size_t mib = argc > 1 ? strtoul(argv[1], nullptr, 0) : 32;
+	const int reps = argc > 2 ? atoi(argv[2]) : 10;
+	const size_t bytes = mib << 20;
+	hipDeviceProp_t prop;
+	CHECK(hipGetDeviceProperties(&prop, 0));
+	uint32_t *sink;
+	void *dst;
+	CHECK(hipMalloc(&sink, 64));
+	CHECK(hipMalloc(&dst, bytes));
+	hipEvent_t a, b;
+	CHECK(hipEventCreate(&a));
+	CHECK(hipEventCreate(&b));
+	printf("{\"MiB\": %zu, \"results\": [", mib);
+	const char *sep = "";
+	for (int kind = 0; kind < 2; ++kind) {
+		void *h = nullptr, *hd = nullptr;
+		CHECK(hipHostMalloc(&h, bytes, kind ? hipHostMallocCoherent : hipHostMallocDefault));
+		memset(h, 0x5A, bytes);
+		CHECK(hipHostGetDevicePointer(&hd, h, 0));
+		const u32x4 *p = (const u32x4 *)hd;
+		for (int shape = 0; shape < 6; ++shape) {
+			float best = 1e30f;
+			for (int r = 0; r < reps + 1; ++r) {
+				CHECK(hipEventRecord(a, 0));
+				switch (shape) {
+				case 0:
+					rows_kernel<true><<<prop.multiProcessorCount, 1024>>>(p, bytes / 128u, sink);
+					break;
+				case 1:
+					rows_kernel<false><<<prop.multiProcessorCount, 1024>>>(p, bytes / 128u, sink);
+					break;
+				case 2:
+					grid_kernel<true><<<(unsigned)(bytes / 16u / 256u), 256>>>(p, bytes / 16u, sink);
+					break;
+				case 3:
+					grid_kernel<false><<<(unsigned)(bytes / 16u / 256u), 256>>>(p, bytes / 16u, sink);
+					break;
+				case 4:
+					grid_x1_kernel<<<(unsigned)(bytes / 4u / 256u), 256>>>((const uint32_t *)hd, bytes / 4u, sink);
+					break;
+				case 5:
+					CHECK(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, 0));
+					break;
+				}
+				CHECK(hipEventRecord(b, 0));
+				CHECK(hipEventSynchronize(b));
+				float ms = 0;
+				CHECK(hipEventElapsedTime(&ms, a, b));
+				if (r > 0 && ms < best)
+					best = ms;
+			}
+			static const char *names[] = {"rows-nt", "rows", "grid-nt", "grid", "grid-x1", "sdma"};
+			printf("%s{\"memory\": \"%s\", \"shape\": \"%s\", \"us\": %.1f, \"GBps\": %.1f}", sep,
+			       kind ? "coherent" : "default", names[shape], best * 1e3, bytes / (best * 1e-3) / 1e9);
+			sep = ", ";
+		}
+		CHECK(hipHostFree(h));
+	}
+	printf("]}\n");
+	return 0;
+}
