@@ -20,9 +20,11 @@
 // hstat (the device view of a coherent pinned host word, or NULL): a flat
 // launch's status word (layout.h PECH_FLAT_PUB / PECH_FLAT_ERR); *flat_tag:
 // that launch's tag, 0 when the batch did not run as one flat launch.
+// host_resident: every buffer is pinned host memory read in place (a
+// zero-copy slot; the flat kernel's interleaved rows, PECH_FLAT_F_IL).
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
 				     size_t ws_bytes, hipStream_t stream, bool small = false, uint32_t *hout = nullptr,
-				     uint64_t *hstat = nullptr, uint64_t *flat_tag = nullptr);
+				     uint64_t *hstat = nullptr, uint64_t *flat_tag = nullptr, bool host_resident = false);
 // The GPUs a multi-device caller spreads over: PECH_DEVICES="0,0,..." (a
 // repeated id puts several shards or contexts on one GPU: how one-GPU boxes
 // rehearse eight) or every visible device.  Count, or a negative errno.

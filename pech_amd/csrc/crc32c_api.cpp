@@ -300,6 +300,13 @@ static uint32_t rpw_min()
 	}();
 	return v;
 }
+// PECH_FLAT_IL=0: host-resident flat launches keep static slices (A/B and
+// tests; read at each such launch)
+static bool flat_il()
+{
+	const char *e = getenv("PECH_FLAT_IL");
+	return !(e && e[0] == '0');
+}
 static std::atomic<uint64_t> g_flat_tag{0};
 static std::once_flag g_flat_tag_init;
 
@@ -329,9 +336,14 @@ static uint64_t flat_tag()
 // (or its publication) in (layout.h PECH_FLAT_ERR / PECH_FLAT_PUB; NULL:
 // the device entry points' word of the context); *flat_tag: the flat
 // launch's tag (0: no flat launch).
+// host_resident: every buffer is pinned host memory the kernel reads in place
+// (an async zero-copy slot): flat launches of uniform large buffers then walk
+// interleaved rows (PECH_FLAT_F_IL), the shape that reads the host link at the
+// copy engines' rate.
 static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
 			size_t ws_bytes, hipStream_t stream, const uint64_t *d_dsts = nullptr, uint32_t *hout = nullptr,
-			bool *published = nullptr, uint64_t *hstat = nullptr, uint64_t *flat_tag_out = nullptr)
+			bool *published = nullptr, uint64_t *hstat = nullptr, uint64_t *flat_tag_out = nullptr,
+			bool host_resident = false)
 {
 	if (flat_tag_out)
 		*flat_tag_out = 0;
@@ -367,7 +379,8 @@ static int launch_batch(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 			const bool pub = hout && m == n; // (one launch: a flat batch is)
 			// test library only: the kernel's fault bits (release: always 0)
 			const uint32_t test = (pech_fault(PECH_FAULT_FLAT_TIMEOUT) ? PECH_FLAT_T_TIMEOUT : 0u) |
-					      (pub && pech_fault(PECH_FAULT_FLAT_NOPUB) ? PECH_FLAT_T_NOPUB : 0u);
+					      (pub && pech_fault(PECH_FAULT_FLAT_NOPUB) ? PECH_FLAT_T_NOPUB : 0u) |
+					      (host_resident && flat_il() ? PECH_FLAT_F_IL : 0u);
 			const uint64_t tag = flat_tag();
 			HIP_TRY(pech_launch_flat(d_descs + off, m, c->d_consts, d_out + off, (uint32_t)c->ncu, rpw_min(),
 						 (uint64_t *)ws, tag, stream, tl.a, tl.b, pub ? hout : nullptr,
@@ -459,7 +472,7 @@ static int launch_small(DevCtx *c, const pech_desc *d_descs, uint32_t *d_out, un
 
 PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, unsigned int n, void *ws,
 				     size_t ws_bytes, hipStream_t stream, bool small, uint32_t *hout, uint64_t *hstat,
-				     uint64_t *flat_tag)
+				     uint64_t *flat_tag, bool host_resident)
 {
 	if (flat_tag)
 		*flat_tag = 0;
@@ -472,7 +485,7 @@ PECH_HIDDEN int pech_internal_launch(const pech_desc *d_descs, uint32_t *d_out, 
 		return hout && n <= PECH_MAX_BATCH ? (launch_small(c, d_descs, hout, n, stream) ?: 1)
 						   : launch_small(c, d_descs, d_out, n, stream);
 	bool pub = false;
-	rc = launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream, nullptr, hout, &pub, hstat, flat_tag);
+	rc = launch_batch(c, d_descs, d_out, n, ws, ws_bytes, stream, nullptr, hout, &pub, hstat, flat_tag, host_resident);
 	return rc ? rc : pub ? 1 : 0;
 }
 

@@ -772,7 +772,8 @@ static int issue_slot(crc32c_async *a, Slot *s)
 	// (rc 1: no copy after them -- a blit kernel and its dispatch, ~4-5 us of
 	// a lone payload's latency, profiles/r05/lat_prof.txt), else copied
 	int rc = pech_internal_launch(descs, s->d_out, m, s->d_ws, pech_ws_bytes(kSlotDescs), s->stream,
-				      s->maxlen < kDirectMax && !a->planned_only, s->out_view, s->stat_view, &s->flat_tag);
+				      s->maxlen < kDirectMax && !a->planned_only, s->out_view, s->stat_view, &s->flat_tag,
+				      s->used == 0 && s->zc_bytes > 0 /* every piece read in place from pinned pages */);
 	if (rc < 0)
 		return fail_slot(a, s, rc);
 	s->published = rc == 1 && s->flat_tag != 0;

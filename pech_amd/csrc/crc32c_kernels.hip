@@ -925,10 +925,14 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 // one window instead of 128 scattered slices (copy probe: 389.5 against
 // 407.0 us per GiB, profiles/r03/copyshape_probe.json).  The cursor is the
 // workgroup's, the same in all its waves.
-template <bool COPY>
+// FLAT (pech_crc32c_flat on host-resident slots, PECH_FLAT_F_IL): the
+// descriptors from the wave's LDS table, the last line's bytes kept below kb.
+template <bool COPY, bool FLAT = false>
 __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
-					uint32_t pos, uint32_t lr, uint32_t rem, uint32_t j, uint32_t g8)
+					uint32_t pos, uint32_t lr, uint32_t rem, uint32_t j, uint32_t g8,
+					const uint32_t *lds = nullptr)
 {
+	static_assert(!(FLAT && COPY), "flat batches: CRC only");
 	Step S;
 	int64_t dl = 0;
 	S.T = 0;
@@ -942,7 +946,7 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 	S.blo = S.bhi = 0;
 #endif
 	if (rem) {
-		const pech_core cd = cores[pos]; // wave-uniform: scalar loads
+		const pech_core cd = FLAT ? flat_core(lds, pos) : cores[pos]; // wave-uniform (scalar loads when planned)
 		const uint32_t rows0 = uni(cd.rows);
 		const uint64_t a0 = uni64(cd.addr);
 		const uint64_t vb0 = a0 & ~(uint64_t)(PECH_ROW_BYTES - 1u);
@@ -968,8 +972,8 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 			S.nl = nn;
 			S.nu = nn;
 			S.oz = PECH_META_ORIG(meta0) | head_bits(st == 0, g8, lb0) | ra_bit(rows0 - last - 1u) |
-			       tail_bits(last == rows0 - 1u, g8, zt0);
-			S.mp = mp_bits(rows0 - last - 1u, meta0);
+			       (FLAT ? tail_of<true>(last == rows0 - 1u, g8, meta0) : tail_bits(last == rows0 - 1u, g8, zt0));
+			S.mp = mp_of<FLAT>(rows0 - last - 1u, meta0);
 		} else {
 			// an idle group reloads the portion's first row (valid memory,
 			// the redirect of row 0's pieces before the buffer kept), ignored
@@ -1310,8 +1314,10 @@ __device__ __forceinline__ bool wave_share(uint32_t Rtot, uint32_t W, uint32_t r
 #endif
 #ifdef PECH_WG_MAJOR_SMALL
 	if (!prop)
-		st.nlive = (uint32_t)min((uint64_t)gridDim.x, ((uint64_t)Rtot + PECH_MAIN_WAVES * rpw - 1u) / (PECH_MAIN_WAVES * rpw));
+#else
+	if (!prop && il) // (interleaved rows keep workgroup-major shares: 16 rpw rows per live workgroup)
 #endif
+		st.nlive = (uint32_t)min((uint64_t)gridDim.x, ((uint64_t)Rtot + PECH_MAIN_WAVES * rpw - 1u) / (PECH_MAIN_WAVES * rpw));
 	if (wg0 >= Rtot)
 		return false; // whole workgroup idle (small batch)
 	// The workgroup's static rows [wg0, wg0 + wg_rows) go to its waves in
@@ -1535,7 +1541,8 @@ __device__ __forceinline__ bool prologue_start(uint32_t *lds, const pech_core *_
 // fill's exact size).  Uniform (every buffer the same rows, none empty):
 // position p holds rows [p U0, (p+1) U0), as the pool needs.
 __device__ __forceinline__ bool prologue_flat(uint32_t *lds, const u32x4 (&dv)[4], uint32_t n, uint32_t lane,
-					      uint32_t wave, uint32_t W, uint32_t rpw_min, Start &st, uint32_t &Rtot)
+					      uint32_t wave, uint32_t W, uint32_t rpw_min, Start &st, uint32_t &Rtot,
+					      bool il_req)
 {
 	uint32_t rows[4], lsum = 0;
 #pragma unroll
@@ -1560,12 +1567,19 @@ __device__ __forceinline__ bool prologue_flat(uint32_t *lds, const u32x4 (&dv)[4
 	for (uint32_t k = 0; k < 4; ++k)
 		uok = uok && (4u * lane + k >= n || rows[k] == U0);
 	const bool uniform = U0 != 0u && __ballot(!uok) == 0ull;
-	if (!wave_share<false>(Rtot, W, rpw_min, wave, uniform, false, st))
+	// host-resident slots (il_req): a uniform batch of buffers of at least
+	// PECH_IL_MIN_ROWS rows walks interleaved rows, as the fused copy does
+	// (the workgroup's 128 groups over one portion, 16 KiB per row step):
+	// GPU reads of pinned host memory in static slices touch 32K pages at
+	// once and reach 45-48 GB/s, interleaved 50-56 GB/s, the copy engines'
+	// rate (tools/host_probe.hip, profiles/r06/host_probe.txt)
+	const bool il = il_req && uniform && U0 >= PECH_IL_MIN_ROWS;
+	if (!wave_share<false>(Rtot, W, rpw_min, wave, uniform, il, st))
 		return false; // whole workgroup idle (small batch)
 	st.U0 = U0;
 	st.p0 = st.lr0 = 0;
 	st.jj = st.pjj = st.nzjj = st.nsjj = 0;
-	if (st.rem_all) {
+	if (st.rem_all && !il) {
 		// the one position p with prefix(p) <= r0 < prefix(p) + rows(p)
 		const uint32_t r0 = st.r0;
 		uint32_t pre = incl - lsum, hk = 4u, lr = 0;
@@ -1969,7 +1983,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 		for (uint32_t j = 0; j < T128; ++j) {
 			t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
-			t16k[j] = COPY || PECH_IL_CRC ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS] : 0u; // interleaved mode's table
+			t16k[j] = COPY || PECH_IL_CRC || (FLAT && !FLATG) ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS]
+									   : 0u; // interleaved mode's table
 		}
 #pragma unroll
 		for (uint32_t k = 0; k < TPT; ++k)
@@ -2089,7 +2104,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			fill_tables(false);
 			live = prologue_flatg(lds, dv, descs, n, tid, lane, wave, W, rpw_min, sv, Rtot, seeds);
 		} else {
-			live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot);
+			live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot, test & PECH_FLAT_F_IL);
 			seeds = __ballot((4u * lane < n && dv[0].w) || (4u * lane + 1u < n && dv[1].w) ||
 					 (4u * lane + 2u < n && dv[2].w) || (4u * lane + 3u < n && dv[3].w)) != 0ull;
 		}
@@ -2183,8 +2198,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 	}
 	Step S;
 	if constexpr (FLAT)
-		S = plan_step<false, false, true, FLATG>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false, pech_core{},
-							 0u, n);
+		S = il ? plan_il<false, true>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8, lds)
+		       : plan_step<false, false, true, FLATG>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false,
+							      pech_core{}, 0u, n);
 	else
 		S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
 		       : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
@@ -2411,8 +2427,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			}
 		}
 #ifndef PECH_NO_NEXT_SPEC
-		const Step N = FLAT ? plan_step<false, false, true, FLATG>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
-									   false, pech_core{}, 0u, n)
+		const Step N = FLAT ? (il ? plan_il<false, true>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8, lds)
+				      : plan_step<false, false, true, FLATG>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
+									     false, pech_core{}, 0u, n))
 			   : il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 			   : COPY ? plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid)
 				  : plan_step<COPY, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid, nspec, nppos);
@@ -2431,8 +2448,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			nspec = load_spec(cores, nppos + grp);
 		}
 #else // A/B: N's descriptors loaded when N is planned
-		const Step N = FLAT ? plan_step<false, false, true, FLATG>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
-									   false, pech_core{}, 0u, n)
+		const Step N = FLAT ? (il ? plan_il<false, true>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8, lds)
+				      : plan_step<false, false, true, FLATG>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
+									     false, pech_core{}, 0u, n))
 			   : il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 				  : plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid);
 #endif

@@ -179,6 +179,10 @@ struct pech_ws {
 /* test library only (crc32c_test_inject): the kernel's fault bits */
 #define PECH_FLAT_T_TIMEOUT 1u /* every wave that waits for out[] times out at once */
 #define PECH_FLAT_T_NOPUB 2u   /* the async slot's publication is skipped */
+/* ... and the library's mode bit: the batch is read from pinned host memory
+ * (an async zero-copy slot): uniform batches of large buffers walk interleaved
+ * rows, the access shape that reads the host link at the copy engines' rate */
+#define PECH_FLAT_F_IL 4u
 
 static inline size_t pech_ws_align(size_t x) { return (x + 255u) & ~(size_t)255u; }
 

@@ -419,3 +419,37 @@ def test_msgr_lone_payloads_route_to_the_host():
         L.crc32c_msgr_conn_destroy(conn)
         ac.close()
     assert released == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("il", ["1", "0"])
+@pytest.mark.parametrize("k,size,off", [(8, 4 << 20, 0), (30, (1 << 20) - 100, 0), (64, 200 << 10, 17), (5, 131072, 0),
+                                        (3, 131072 - 1, 64), (40, 1 << 20, 4095)])
+def test_zero_copy_slots_interleaved_rows(monkeypatch, il, k, size, off):
+    """Zero-copy slots of uniform payloads of >= 128 KiB (pinned crc32c_pages
+    memory read in place) run the flat kernel on interleaved rows
+    (PECH_FLAT_F_IL, crc32c_kernels.hip prologue_flat): the workgroup's 128
+    lane groups over one portion, A_16384 Horner steps, the last line's bytes
+    kept below kb, every byte offset within the line; PECH_FLAT_IL=0 keeps the
+    static slices.  Every CRC against the oracle, seeds included."""
+    import pech_amd as P
+
+    monkeypatch.setenv("PECH_FLAT_IL", il)  # (read at each zero-copy flat launch)
+    rng = np.random.default_rng(k * 1000 + size % 997 + off)
+    order = max(0, int(np.ceil(np.log2((size + off) / 4096))))
+    pages = [P.Pages(order) for _ in range(k)]
+    ac = P.AsyncCrc()
+    got, want = {}, {}
+    try:
+        for i, pg in enumerate(pages):
+            pg.view[off:off + size] = rng.integers(0, 256, size, dtype=np.uint8)
+            seed = int(rng.integers(0, 1 << 32)) if i % 3 == 1 else 0
+            want[i] = O.crc(seed, pg.view[off:off + size])
+            ac.submit(pg.ptr + off, size, seed, lambda crc, err, i=i: got.__setitem__(i, (crc, err)))
+        ac.flush()
+        _wait_all(ac)
+        assert got == {i: (want[i], 0) for i in range(k)}
+    finally:
+        ac.close()
+        for pg in pages:
+            pg.free()
