@@ -945,7 +945,15 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 #ifdef PECH_DEBUG_BOUNDS
 	S.blo = S.bhi = 0;
 #endif
-	if (rem) {
+	// A portion of at most j0 rows (the wave's first group) gives the whole
+	// wave nothing to do: it moves on to the next portion instead of ending
+	// its walk -- the workgroup's range goes on, and a range that starts in a
+	// buffer's last rows (P < 120) left waves 1-15 without their rows of every
+	// later portion (fused copy and flat interleaved mode; found by
+	// test_zero_copy_slots_interleaved_rows: 3 x 1,025-row buffers, a range
+	// starting 4 rows before a buffer's end)
+	const uint32_t j0 = j & ~7u;
+	while (rem) {
 		const pech_core cd = FLAT ? flat_core(lds, pos) : cores[pos]; // wave-uniform (scalar loads when planned)
 		const uint32_t rows0 = uni(cd.rows);
 		const uint64_t a0 = uni64(cd.addr);
@@ -954,11 +962,20 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 		const uint32_t meta0 = uni(cd.meta);
 		const uint32_t zt0 = PECH_META_ZT(meta0);
 		const uint32_t P = min(rows0 - lr, rem);
+		if (P <= j0) { // no row of this portion for any group of the wave
+			rem -= P;
+			if (lr + P == rows0) {
+				++pos;
+				lr = 0;
+			} else {
+				lr += P;
+			}
+			continue;
+		}
 		const uint32_t nn = P > j ? (P - j + PECH_IL_GROUPS - 1u) / PECH_IL_GROUPS : 0u;
 		const uint32_t st = lr + j;
 		// the wave's 8 groups are j0..j0+7: counts nonincreasing in the group
-		const uint32_t j0 = j & ~7u;
-		S.T = P > j0 ? (P - j0 + PECH_IL_GROUPS - 1u) / PECH_IL_GROUPS : 0u;
+		S.T = (P - j0 + PECH_IL_GROUPS - 1u) / PECH_IL_GROUPS;
 		uint32_t tmin = S.T;
 #pragma unroll
 		for (uint32_t g = 1; g < 8; ++g) {
@@ -993,6 +1010,7 @@ __device__ __forceinline__ Step plan_il(const pech_core *__restrict__ cores, con
 		} else {
 			lr += P;
 		}
+		break;
 	}
 	S.pos = pos;
 	S.lr = lr;

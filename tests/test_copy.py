@@ -133,6 +133,8 @@ def test_copy_huge_buffer_misaligned(torch_dev):
     ((1 << 17) + 5, 300, 3, 11),         # 1,025 rows each, unaligned sources and destinations
     ((1 << 17) - 16, 513, 16, 1),        # just below and around the threshold of the mode
     ((6 << 20) + 99, 3, 7, 0),           # few buffers, many workgroups each
+    (1025 * 128 - 100, 300, 0, 0),       # workgroup ranges that start 4 rows before a buffer's end (round 6)
+    (1025 * 128 - 100, 3, 64, 5),        # ... and the small-launch ranges of 3 buffers
 ])
 def test_copy_uniform_large_buffers(torch_dev, size, n, soff, doff):
     # uniform batches of large buffers take the fused copy's interleaved mode
@@ -140,7 +142,10 @@ def test_copy_uniform_large_buffers(torch_dev, size, n, soff, doff):
     # CRC and every destination byte, guards intact
     torch, dev = torch_dev
     rng = np.random.default_rng(size + n)
-    stride_s, stride_d = size + 4096, size + 8192
+    # strides that are whole lines: every buffer has the same alignment, so
+    # the same rows -- a uniform batch (until round 6 the strides were size +
+    # 4 KiB, which left only the first case uniform)
+    stride_s, stride_d = (size + 4096 + 127) // 128 * 128, size + 8192
     src_offs = soff + stride_s * np.arange(n, dtype=np.int64)  # the same alignment for every buffer: uniform
     dst_offs = doff + stride_d * np.arange(n, dtype=np.int64)
     lens = np.full(n, size, np.int64)
