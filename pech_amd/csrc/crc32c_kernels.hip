@@ -1935,7 +1935,7 @@ __device__ __forceinline__ void flat_publish(uint64_t *flag, uint32_t nlive, uin
 	}
 }
 
-template <bool COPY, uint32_t U, bool FLAT = false, bool FLATG = false>
+template <bool COPY, uint32_t U, bool FLAT = false, bool FLATG = false, bool FIL = false>
 __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__restrict__ cores,
 					  const uint32_t *__restrict__ lrs, const uint32_t *__restrict__ partials,
 					  const uint32_t *__restrict__ nzs, uint32_t n,
@@ -1946,6 +1946,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 {
 	static_assert(!(FLAT && COPY), "flat batches: CRC only");
 	static_assert(FLAT || !FLATG, "FLATG is a flat mode");
+	static_assert(!FIL || (FLAT && !FLATG), "FIL: the flat kernel's interleaved-rows variant");
 	constexpr uint32_t NMAX = FLATG ? PECH_FLATG_MAX : PECH_FLAT_MAX; // flat: the launch's batch limit
 	const uint32_t tid = threadIdx.x;
 	// flat steps read {addr, rows, meta} per position: FLATG from the caller's
@@ -2001,7 +2002,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #pragma unroll
 		for (uint32_t j = 0; j < T128; ++j) {
 			t128[j] = consts[PECH_C_TAB128 + tid + j * PECH_MAIN_THREADS];
-			t16k[j] = COPY || PECH_IL_CRC || (FLAT && !FLATG) ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS]
+			t16k[j] = COPY || PECH_IL_CRC || FIL ? consts[PECH_C_TAB16K + tid + j * PECH_MAIN_THREADS]
 									   : 0u; // interleaved mode's table
 		}
 #pragma unroll
@@ -2122,7 +2123,7 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			fill_tables(false);
 			live = prologue_flatg(lds, dv, descs, n, tid, lane, wave, W, rpw_min, sv, Rtot, seeds);
 		} else {
-			live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot, test & PECH_FLAT_F_IL);
+			live = prologue_flat(lds, dv, n, lane, wave, W, rpw_min, sv, Rtot, FIL && (test & PECH_FLAT_F_IL));
 			seeds = __ballot((4u * lane < n && dv[0].w) || (4u * lane + 1u < n && dv[1].w) ||
 					 (4u * lane + 2u < n && dv[2].w) || (4u * lane + 3u < n && dv[3].w)) != 0ull;
 		}
@@ -2176,7 +2177,9 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #endif
 	const uint32_t U0 = sv.U0, wg_rows = sv.wg_rows, r0 = sv.r0, r1 = sv.r1, jmax = sv.jmax;
 	const uint64_t wg0 = sv.wg0;
-	const bool il = sv.il;
+	// (the plain flat kernel never interleaves: a compile-time false keeps its
+	// row stride an immediate -- a runtime one cost ~4 us per launch)
+	const bool il = FLAT && !FIL ? false : sv.il;
 	const uint32_t rsb = il ? PECH_IL_GROUPS * PECH_ROW_BYTES : PECH_ROW_BYTES; // bytes from one row of a run to the next
 	uint32_t rem_all = sv.rem_all, p0 = sv.p0, lr0 = sv.lr0;
 	const uint32_t jj = sv.jj, pjj = sv.pjj, nzjj = sv.nzjj, nsjj = sv.nsjj;
@@ -2626,6 +2629,19 @@ extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_f
 				       tag, hout, hstat, test);
 }
 
+// pech_crc32c_flat for host-resident batches (PECH_FLAT_F_IL: the async
+// layer's zero-copy slots): uniform batches of rows >= PECH_IL_MIN_ROWS walk
+// interleaved rows (plan_il), others static shares, as pech_crc32c_flat
+extern "C" __global__ __launch_bounds__(PECH_MAIN_THREADS, 1) void pech_crc32c_flat_il(
+	const pech_desc *__restrict__ descs, uint32_t n, const uint32_t *__restrict__ consts, uint32_t *__restrict__ out,
+	uint32_t rpw_min, uint64_t *__restrict__ flag, uint64_t tag, uint32_t *__restrict__ hout, uint64_t *hstat,
+	uint32_t test)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t lds[L_BYTES / 4u];
+	main_body<false, PECH_U, true, false, true>(lds, nullptr, nullptr, nullptr, nullptr, n, consts, out, rpw_min, nullptr,
+						    descs, flag, tag, hout, hstat, test);
+}
+
 // The same for PECH_FLAT_MAX < n <= PECH_FLATG_MAX buffers (the messenger's
 // slots of 64 KiB payloads, 512 to a 32 MiB slot; C4's 64 KiB class, 4,096
 // per 256 MiB launch): one launch instead of plan + main.  Its prologue
@@ -3073,7 +3089,10 @@ extern "C" hipError_t pech_launch_flat(const pech_desc *descs, uint32_t n, const
 {
 	if (n == 0 || n > PECH_FLATG_MAX || ((uintptr_t)flag & 7u))
 		return hipErrorInvalidValue;
-	if (n <= PECH_FLAT_MAX)
+	if (n <= PECH_FLAT_MAX && (test & PECH_FLAT_F_IL))
+		hipExtLaunchKernelGGL(pech_crc32c_flat_il, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop,
+				      0u, descs, n, consts, out, rpw_min, flag, tag, hout, hstat, test);
+	else if (n <= PECH_FLAT_MAX)
 		hipExtLaunchKernelGGL(pech_crc32c_flat, dim3(ncu), dim3(PECH_MAIN_THREADS), 0, stream, ev_start, ev_stop, 0u,
 				      descs, n, consts, out, rpw_min, flag, tag, hout, hstat, test);
 	else
@@ -3101,6 +3120,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.33 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) ",flatg<=" PECH_STR(PECH_FLATG_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.33 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) "(host:il),flatg<=" PECH_STR(PECH_FLATG_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }

@@ -44,7 +44,8 @@ def kernel_body(asm, name):
 
 @pytest.mark.parametrize("kernel", ["pech_crc32c_plan", "pech_crc32c_main", "pech_crc32c_plan_copy",
                                     "pech_crc32c_main_copy", "pech_crc32c_small", "pech_crc32c_direct",
-                                    "pech_crc32c_direct_copy", "pech_crc32c_flat", "pech_crc32c_flatg"])
+                                    "pech_crc32c_direct_copy", "pech_crc32c_flat", "pech_crc32c_flat_il",
+                                    "pech_crc32c_flatg"])
 def test_no_calls_no_scratch(device_asm, kernel):
     asm, _ = device_asm
     body = kernel_body(asm, kernel)
@@ -53,7 +54,8 @@ def test_no_calls_no_scratch(device_asm, kernel):
 
 
 @pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct",
-                                    "pech_crc32c_direct_copy", "pech_crc32c_flat", "pech_crc32c_flatg"])
+                                    "pech_crc32c_direct_copy", "pech_crc32c_flat", "pech_crc32c_flat_il",
+                                    "pech_crc32c_flatg"])
 def test_main_kernel_register_budget(device_asm, kernel):
     _, remarks = device_asm
     m = re.search(r"Function Name: %s \[.*?VGPRs: (\d+).*?ScratchSize \[bytes/lane\]: (\d+)" % kernel, remarks,
@@ -88,7 +90,8 @@ def _blocks(body):
     return out
 
 
-@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_direct", "pech_crc32c_flat", "pech_crc32c_flatg"])
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_direct", "pech_crc32c_flat", "pech_crc32c_flat_il",
+                                    "pech_crc32c_flatg"])
 def test_row_loops_never_drain_the_ring(device_asm, kernel):
     """The row loops (basic blocks with a full block of Horner steps and
     their prefetch loads) keep PECH_U-1 loads in flight across the back
@@ -128,7 +131,7 @@ def _loop_regions(body):
     return out
 
 
-@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_flat", "pech_crc32c_flatg"])
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_flat", "pech_crc32c_flat_il", "pech_crc32c_flatg"])
 def test_loops_with_ring_loads_never_wait_for_zero(device_asm, kernel):
     """Loop-level form of the check: every loop of the CRC kernel that issues
     ring loads has only counted vmcnt waits."""
