@@ -306,7 +306,7 @@ def main():
     traffic = None
     tag = args.config + ("-copy" if dsts else "")
     for pj in ([args.profile_json] if args.profile_json else
-               [os.path.join(REPO, "profiles", r, f"{tag}_traffic.json") for r in ("r05", "r04", "r03", "r02", "r01")]):
+               [os.path.join(REPO, "profiles", r, f"{tag}_traffic.json") for r in ("r06", "r05", "r04", "r03", "r02", "r01")]):
         if os.path.exists(pj):
             prof = json.load(open(pj))
             if prof.get("kernel") == P.version():
