@@ -294,14 +294,12 @@ __device__ __forceinline__ void plan_body(const pech_desc *__restrict__ descs, u
 	const uint64_t safe = (uint64_t)(descs + min(b, n - 1u));
 	const uint64_t end = d.addr + d.len, ce = end & ~(uint64_t)15, a0 = d.addr & ~(uint64_t)15;
 	const bool needT = d.len != 0 && (end & 15u) != 0;
-	// Both block loads wait for the descriptor: a second round trip on the
-	// plan's critical path, taken only by waves with a lane that needs one
-	// (wave-uniform branches; vT / vA are read only under needT / hp)
-	u32x4 vT = (u32x4)(0u), vA = (u32x4)(0u);
-	if (__ballot(needT) != 0ull)
-		vT = *(g_u32x4 *)(needT ? ce : safe);
+	// (skipping this round trip in waves without an unaligned end measured
+	// neutral on c4-64k / C4 steps: profiles/r06/ab_copy_plan.txt)
+	const u32x4 vT = *(g_u32x4 *)(needT ? ce : safe);
+	u32x4 vA = (u32x4)(0u);
 	const bool hp = COPY && d.len != 0 && (d.addr & 15u) != 0 && a0 != ce; // partial first piece of a core
-	if (COPY && __ballot(hp) != 0ull)
+	if (COPY)
 		vA = *(g_u32x4 *)(hp ? a0 : safe);
 	if (tid < 256)
 		t1[tid] = tv1;
