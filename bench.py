@@ -94,7 +94,7 @@ def parse():
                     help="device entry point: planned = crc32c_dev_batch_ws_async (plan + main kernel), small = "
                          "crc32c_dev_batch_small_async (direct kernel, one launch); auto = small when every buffer "
                          "is below 32 KiB, as the async layer routes its slots")
-    ap.add_argument("--flat-max", type=int, default=256,
+    ap.add_argument("--flat-max", type=int, default=4096,
                     help="device batches of at most this many buffers run as one launch with no plan kernel "
                          "(crc32c_set_flat_max; 0 = always plan + main, the A/B against the planned path)")
     ap.add_argument("--no-kernel-events", action="store_true",

@@ -144,9 +144,8 @@ int crc32c_dev_copy_batch_small_async(const struct crc32c_desc *d_descs, const u
  * synchronous and async host paths launch) of at most n buffers run as ONE
  * kernel launch with no plan kernel; larger ones, fused copies and batches
  * captured in a graph take the two-launch plan + main path (pech_crc32c_flat
- * up to 256 buffers, pech_crc32c_flatg up to 4,096).  Default 256 (the
- * larger kernel saves the plan launch but its workgroup-wide prologue costs
- * about as much: DESIGN.md §6.7), maximum 4,096; 0 = always plan + main.
+ * up to 256 buffers, pech_crc32c_flatg up to 4,096).  Default and maximum
+ * 4,096; 0 = always plan + main.
  * Results are identical either way.  Returns the previous value. */
 unsigned int crc32c_set_flat_max(unsigned int n);
 

@@ -43,7 +43,7 @@ def set_cpu_max(nbytes):
 def set_flat_max(n):
     """Device batches of at most n buffers run as one launch with no plan
     kernel (pech_crc32c_flat up to 256, pech_crc32c_flatg up to 4,096;
-    default 256, maximum 4,096, 0 = always plan + main).  Returns the previous value (0 from a pre-flat release loaded
+    default and maximum 4,096, 0 = always plan + main).  Returns the previous value (0 from a pre-flat release loaded
     for an A/B, which always plans)."""
     fn = getattr(lib(), "crc32c_set_flat_max", None)
     return int(fn(int(n))) if fn is not None else 0

@@ -282,12 +282,12 @@ static bool capturing(hipStream_t s)
 // counter from a per-process start, so a tag left in recycled memory by
 // another run does not match either.  A graph replays its captured tag, so
 // captured batches take plan + main.
-// Default PECH_FLAT_MAX (256): pech_crc32c_flatg (up to PECH_FLATG_MAX
-// buffers) is opt-in through crc32c_set_flat_max -- its workgroup-wide
-// prologue costs what the plan launch it saves did, so the one-stream step is
-// no faster (32 MiB of 64 KiB buffers 17.8 -> 19.5 us, 256 MiB 56.6 -> 56.9 us,
-// profiles/r06/flatg.txt), while two streams gain 7 % on C4's 64 KiB class.
-static std::atomic<unsigned int> g_flat_max{PECH_FLAT_MAX};
+// Default PECH_FLATG_MAX (4,096): since its prologue locates a uniform
+// batch's shares by division and its first step plans from descriptors
+// loaded at entry, pech_crc32c_flatg's one launch costs what plan + main did
+// on one stream (c4-64k 4,628 / 4,625 against 4,630 / 4,624 GiB/s serial) and
+// two streams gain 6-7 % (5,549-5,610 against 5,247-5,256; profiles/r06/flatg.txt).
+static std::atomic<unsigned int> g_flat_max{PECH_FLATG_MAX};
 
 // rows per wave below which a launch spreads its shares wave-major
 // (crc32c_kernels.hip wave_share); PECH_RPW_MIN overrides it (A/B measurements)

@@ -655,15 +655,18 @@ __device__ __forceinline__ pech_core flat_core(const uint32_t *lds, uint32_t p)
 // crc32c_desc array, L2-resident after the prologue read it), by SCALAR loads
 // at wave-uniform positions (lgkmcnt: the ring's vector loads are never
 // drained for them), each turned into the LDS table's {addr, rows, meta}.
-__device__ __forceinline__ pech_core flatg_core(const pech_core *__restrict__ g, uint32_t p)
+__device__ __forceinline__ pech_core flatg_conv(u32x4 v, uint32_t p) // v: {addr lo, addr hi, len, seed}
 {
-	const u32x4 v = ((const u32x4 *)g)[uni(p)]; // {addr lo, addr hi, len, seed}
 	pech_core c;
 	c.addr = ((uint64_t)v.y << 32) | v.x;
 	const uint32_t lb = v.x & (PECH_ROW_BYTES - 1u), len = v.z;
 	c.rows = len ? (uint32_t)(((uint64_t)lb + len + PECH_ROW_BYTES - 1u) >> 7) : 0u;
 	c.meta = p | (c.rows ? c.rows * PECH_ROW_BYTES - lb - len : 0u) << 20; // (T mod 2^32: exact, < 128)
 	return c;
+}
+__device__ __forceinline__ pech_core flatg_core(const pech_core *__restrict__ g, uint32_t p)
+{
+	return flatg_conv(((const u32x4 *)g)[uni(p)], p);
 }
 
 // Step.oz bits of lane g8 for a run that ends its buffer (last): the zl flag
@@ -692,14 +695,15 @@ __device__ __forceinline__ uint32_t mp_of(uint32_t ra, uint32_t meta)
 // FLAT: the descriptors come from the wave's LDS table (flat_core) for
 // positions < nflat, empty buffers included (skipped here).
 // FLATG: the same from the caller's descriptors (`cores` is then the
-// crc32c_desc array; flatg_core).
+// crc32c_desc array; flatg_core); with PRE, `spec` holds position ppos + grp
+// already converted (flatg_conv).
 template <bool COPY, bool PRE = false, bool FLAT = false, bool FLATG = false>
 __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, const int64_t *__restrict__ deltas,
 					  const uint32_t *lds, uint32_t pos, uint32_t lr, uint32_t rem, uint32_t lane,
 					  uint32_t g8, uint32_t grp, bool grid, const pech_core &spec = pech_core{},
 					  uint32_t ppos = 0, uint32_t nflat = 0)
 {
-	static_assert(!(FLAT && (COPY || PRE)), "flat batches: CRC only, descriptors from LDS");
+	static_assert(!(FLAT && (COPY || (PRE && !FLATG))), "flat batches: CRC only, descriptors from LDS (flatg: or speculated)");
 	Step S;
 	int64_t dl = 0;
 	S.T = 0;
@@ -736,7 +740,7 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 		const bool hit = PRE && pos == ppos; // wave-uniform
 		pech_core cd;
 		if (FLATG)
-			cd = flatg_core(cores, pos);
+			cd = hit ? spec : flatg_core(cores, pos); // (hit: uni() below reads lane 0, group 0's = pos)
 		else if (FLAT)
 			cd = flat_core(lds, pos);
 		else if (hit)
@@ -744,7 +748,12 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 		else
 			cd = cores[pos];
 #ifdef PECH_DEBUG_BOUNDS
-		if (hit && (cd.rows != cores[pos + grp].rows || cd.addr != cores[pos + grp].addr))
+		if (FLATG && hit) {
+			const uint32_t pj = min(pos + grp, nflat - 1u);
+			const pech_core e = flatg_conv(((const u32x4 *)cores)[pj], pj);
+			if (spec.rows != e.rows || spec.addr != e.addr || spec.meta != e.meta)
+				printf("PECH OOB speculated flatg descriptor pos %u grp %u\n", pos, grp);
+		} else if (hit && (cd.rows != cores[pos + grp].rows || cd.addr != cores[pos + grp].addr))
 			printf("PECH OOB preloaded descriptor pos %u grp %u\n", pos, grp);
 #endif
 		const uint32_t rows0 = uni(cd.rows);
@@ -802,7 +811,12 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 			// workspace memory); such entries are never used.
 			uint32_t vlo = 0, vhi = 0, mrows = 0, mmeta = 0;
 			int64_t mdl = 0;
-			if (FLATG) { // scalar loads of the 8 positions, each group taking its own
+			if (FLATG && hit) { // each group its own speculated entry
+				vlo = (uint32_t)spec.addr;
+				vhi = (uint32_t)(spec.addr >> 32);
+				mrows = spec.rows;
+				mmeta = spec.meta;
+			} else if (FLATG) { // scalar loads of the 8 positions, each group taking its own
 #pragma unroll
 				for (uint32_t j = 0; j < 8; ++j) {
 					const pech_core dj = flatg_core(cores, min(pos + j, nflat - 1u));
@@ -1700,7 +1714,11 @@ __device__ __forceinline__ bool prologue_flatg(uint32_t *lds, const u32x4 (&dv)[
 	st.U0 = U0;
 	st.p0 = st.lr0 = 0;
 	st.jj = st.pjj = st.nzjj = st.nsjj = 0;
-	if (st.rem_all) {
+	if (st.rem_all && uniform) {
+		// position p holds rows [p U0, (p+1) U0): no search, no loads
+		st.p0 = st.r0 / U0;
+		st.lr0 = st.r0 - st.p0 * U0;
+	} else if (st.rem_all) {
 		const uint32_t r0 = st.r0;
 		// threads whose prefix is <= r0: the last of them holds r0 (a thread
 		// with no rows before it shares the next one's prefix, which is > r0)
@@ -1711,10 +1729,9 @@ __device__ __forceinline__ bool prologue_flatg(uint32_t *lds, const u32x4 (&dv)[
 			cnt += (woff + v.x <= r0) + (woff + v.y <= r0) + (woff + v.z <= r0) + (woff + v.w <= r0);
 		}
 		const uint32_t ts = lane_value(wave_incl_scan(cnt), 63) - 1u;
-		uint32_t acc = lds[L_FLAT / 4u + ts];
-		for (uint32_t w = 0; w < (ts >> 6); ++w)
-			acc += lds[L_SCAN / 4u + w];
-		acc = uni(acc);
+		// + the waves before ts's: lane ts / 16's woff (its 16 threads are ts's wave's)
+		const uint32_t acc0 = uni(lds[L_FLAT / 4u + ts] + lane_value(woff, ts >> 4));
+		uint32_t acc = acc0;
 		uint32_t p0 = 4u * ts, lr0 = 0;
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k) { // scalar loads: the thread's four descriptors
@@ -2017,12 +2034,17 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #endif
 	uint32_t rows0 = 0, pg = 0, cg = 0, lrg = 0;
 	pech_core spec = pech_core{};
-	u32x4 lr4[4], dv[4];
+	u32x4 lr4[4], dv[4], gspec = (u32x4)(0u);
 	if constexpr (FLATG) {
 		// the batch's descriptors, 4 per THREAD of the workgroup (64 contiguous bytes), with the tables
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k)
 			dv[k] = ((const u32x4 *)descs)[min(4u * tid + k, n - 1u)];
+		// and the first step's, one per lane group, at the likely start
+		// position (exact for uniform batches, as the planned kernel's spec):
+		// the step after the prologue's barrier then plans without a load
+		pg = uni(min((uint32_t)((double)(blockIdx.x * PECH_MAIN_WAVES + wave) * (double)n / (double)W), n - 1u));
+		gspec = ((const u32x4 *)descs)[min(pg + grp, n - 1u)];
 	} else if constexpr (FLAT) {
 		// the batch's descriptors, 4 per lane (64 contiguous bytes), with the tables
 #pragma unroll
@@ -2220,9 +2242,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		rem_all = wg_rows;
 	}
 	Step S;
-	if constexpr (FLAT)
+	if constexpr (FLATG)
+		S = plan_step<false, true, true, true>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false,
+						       flatg_conv(gspec, min(pg + grp, n - 1u)), pg, n);
+	else if constexpr (FLAT)
 		S = il ? plan_il<false, true>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8, lds)
-		       : plan_step<false, false, true, FLATG>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false,
+		       : plan_step<false, false, true, false>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false,
 							      pech_core{}, 0u, n);
 	else
 		S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
