@@ -9,13 +9,14 @@ FETCH_SIZE/WRITE_SIZE are reported in KiB.  On gfx950 FETCH_SIZE counts
 exactly half of the bytes of a wide (16 B/lane) coalesced streaming read, and
 WRITE_SIZE reads the bytes exactly for 16-B-per-lane streaming stores
 (MI355X_MICROARCH.md, HBM section): bytes = FETCH x 1024 x 2 + WRITE x 1024.
-Averaged over every pech_crc32c_main / _main_copy / _direct dispatch (one of them per run).
+Averaged over every dispatch of the config's main kernel (main / main_copy / direct / flat / flatg; one of them per run).
 """
 import csv
 import json
 import sys
 
-KERNELS = ("pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct", "pech_crc32c_direct_copy", "pech_crc32c_flat")
+KERNELS = ("pech_crc32c_main", "pech_crc32c_main_copy", "pech_crc32c_direct", "pech_crc32c_direct_copy", "pech_crc32c_flat",
+           "pech_crc32c_flat_il", "pech_crc32c_flatg")
 
 
 def per_launch_kib(path, counter):
