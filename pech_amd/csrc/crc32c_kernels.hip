@@ -1693,22 +1693,22 @@ __device__ __forceinline__ bool prologue_flatg(uint32_t *lds, const u32x4 (&dv)[
 #ifdef PECH_STAMPS
 	st.t_scan = t_scan;
 #endif
-	// every lane reads the 16 waves' words (broadcast LDS reads)
-	uint32_t tot = 0, woff = 0, umin = 0xFFFFFFFFu, umax = 0, anysd = 0;
-	const uint32_t lw = lane >> 2; // the wave of threads 16 lane .. 16 lane + 15
-#pragma unroll
-	for (uint32_t w = 0; w < PECH_MAIN_WAVES; ++w) {
-		const uint32_t t = lds[L_SCAN / 4u + w];
-		woff += w < lw ? t : 0u;
-		tot += t;
-		umin = min(umin, lds[L_SCAN / 4u + 16u + w]);
-		umax = max(umax, lds[L_SCAN / 4u + 32u + w]);
-		anysd |= lds[L_SCAN / 4u + 48u + w];
-	}
-	Rtot = uni(tot);
-	seeds = uni(anysd) != 0u;
-	const uint32_t U0 = uni(umin);
-	const bool uniform = U0 != 0u && U0 == uni(umax);
+	// one LDS word per lane (lanes 0-15 the waves' totals, 16-31 their
+	// smallest and 32-47 their largest rows, 48-63 their seed flags) and lane
+	// operations: 64 broadcast reads per wave, all 16 waves at once behind the
+	// barrier, kept the LDS pipe busy ~0.8 us
+	const uint32_t sw = lds[L_SCAN / 4u + lane];
+	const uint32_t tw = lane < PECH_MAIN_WAVES ? sw : 0u;
+	const uint32_t tinc = wave_incl_scan(tw);
+	Rtot = lane_value(tinc, PECH_MAIN_WAVES - 1u);
+	// the waves before the one of threads 16 lane .. 16 lane + 15 (lane >> 2)
+	const uint32_t woff = (uint32_t)__shfl((int)(tinc - tw), (int)(lane >> 2));
+	seeds = __ballot(lane >= 48u && sw != 0u) != 0ull;
+	// uniform: every wave holding positions has min = max = wave 0's min
+	const uint32_t nw = (n + 255u) >> 8, m0 = lane_value(sw, 16u);
+	const bool mine = (lane >= 16u && lane < 16u + nw) || (lane >= 32u && lane < 32u + nw);
+	const bool uniform = m0 != 0u && __ballot(mine && sw != m0) == 0ull;
+	const uint32_t U0 = uniform ? m0 : uni(wave_min_u32(lane >= 16u && lane < 32u ? sw : 0xFFFFFFFFu));
 	if (!wave_share<false>(Rtot, W, rpw_min, wave, uniform, false, st))
 		return false; // whole workgroup idle (small batch)
 	st.U0 = U0;

@@ -4,16 +4,20 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 stop() { echo "stopping after rc=$1 ($2)"; exit "$1"; }
+if [ -z "${SKIP_DBG:-}" ]; then
 PECH_CRC32C_LIB=build/lib_dbg.so timeout -k 10 400 python -u -m pytest tests/test_gpu_flat.py tests/test_gpu_bounds.py -x -q \
   --timeout 150 --timeout-method thread > gpurun_out/flatg_dbg.log 2>&1 || { tail -30 gpurun_out/flatg_dbg.log; stop 1 dbg; }
 echo "dbg: $(tail -1 gpurun_out/flatg_dbg.log) oob=$(grep -c 'PECH OOB' gpurun_out/flatg_dbg.log)"
 grep -q "PECH OOB" gpurun_out/flatg_dbg.log && { grep "PECH OOB" gpurun_out/flatg_dbg.log | head; stop 1 oob; }
+fi
+for sl in ${STAMP_LIBS:-build/lib_stamps.so}; do
 for cfg in ${STAMPS:-4096x64k 512x64k}; do
   for fm in ${STAMP_FMS:-4096 0}; do
-    PECH_FLAT_MAX=$fm PECH_CRC32C_LIB=build/lib_stamps.so timeout -k 10 120 python tools/wave_stamps.py $cfg \
-      > gpurun_out/stamps_flatg_${cfg}_$fm.txt 2>&1 || stop $? "stamps $cfg"
-    echo "== $cfg flat_max=$fm"; grep -v "amdgpu.ids\|^xcc\|histogram" gpurun_out/stamps_flatg_${cfg}_$fm.txt
+    PECH_FLAT_MAX=$fm PECH_CRC32C_LIB=$sl timeout -k 10 120 python tools/wave_stamps.py $cfg \
+      > gpurun_out/stamps_flatg_$(basename $sl .so)_${cfg}_$fm.txt 2>&1 || stop $? "stamps $cfg"
+    echo "== $(basename $sl) $cfg flat_max=$fm"; grep -v "amdgpu.ids\|^xcc\|histogram" gpurun_out/stamps_flatg_$(basename $sl .so)_${cfg}_$fm.txt
   done
+done
 done
 for pass in 1 2; do
   for lib in ${LIBS:-pech_amd/libpech_crc32c.so}; do
