@@ -816,16 +816,17 @@ __device__ __forceinline__ Step plan_step(const pech_core *__restrict__ cores, c
 				vhi = (uint32_t)(spec.addr >> 32);
 				mrows = spec.rows;
 				mmeta = spec.meta;
-			} else if (FLATG) { // scalar loads of the 8 positions, each group taking its own
-#pragma unroll
-				for (uint32_t j = 0; j < 8; ++j) {
-					const pech_core dj = flatg_core(cores, min(pos + j, nflat - 1u));
-					const bool mine = grp == j;
-					vlo = mine ? (uint32_t)dj.addr : vlo;
-					vhi = mine ? (uint32_t)(dj.addr >> 32) : vhi;
-					mrows = mine ? dj.rows : mrows;
-					mmeta = mine ? dj.meta : mmeta;
-				}
+			} else if (FLATG) {
+				// each group its own entry by a vector load (a miss: the
+				// planner's prefetch a step ahead normally hits).  Eight scalar
+				// loads and selects here made the compiler schedule the row
+				// loops' lookups one pair at a time (c4-64k 53.3 -> ~49 us)
+				const uint32_t pj = min(pos + grp, nflat - 1u);
+				const pech_core dj = flatg_conv(((const u32x4 *)cores)[pj], pj);
+				vlo = (uint32_t)dj.addr;
+				vhi = (uint32_t)(dj.addr >> 32);
+				mrows = dj.rows;
+				mmeta = dj.meta;
 			} else if (FLAT) { // each group its own entry (LDS: no scalar-load selects)
 				const pech_core dj = flat_core(lds, min(pos + grp, nflat - 1u));
 				vlo = (uint32_t)dj.addr;
@@ -2263,6 +2264,14 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 #ifndef PECH_NEXT_SPEC_FIRST
 	uint32_t nppos = 0xFFFFFFFFu; // (the first step's successor plans with loads)
 	pech_core nspec = pech_core{};
+	// flatg: the raw descriptors where the first step ends, from the start
+	// (a miss in its planner is a vector load, which waits behind the ring);
+	// converted when used (flatg_conv)
+	u32x4 nspec_g = (u32x4)(0u);
+	if constexpr (FLATG) {
+		nppos = min(S.pos, n - 1u);
+		nspec_g = ((const u32x4 *)descs)[min(nppos + grp, n - 1u)];
+	}
 #else // A/B: prefetched from the first step on
 	uint32_t nppos = COPY ? 0u : min(S.pos, nslots - 1u);
 	pech_core nspec = COPY ? pech_core{} : load_spec(cores, nppos + grp);
@@ -2475,14 +2484,21 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 			}
 		}
 #ifndef PECH_NO_NEXT_SPEC
-		const Step N = FLAT ? (il ? plan_il<false, true>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8, lds)
-				      : plan_step<false, false, true, FLATG>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
+		// (flatg: as the planned kernel, from descriptors prefetched by
+		// vector loads a step ahead; its scalar loads for the N of every
+		// step made the row loops' schedule serialise their LDS lookups,
+		// c4-64k 53.3 against 48.9 us for the planned main)
+		const Step N = FLATG ? plan_step<false, true, true, true>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp, false,
+									 flatg_conv(nspec_g, min(nppos + grp, n - 1u)), nppos, n)
+			       : FLAT ? (il ? plan_il<false, true>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8, lds)
+				      : plan_step<false, false, true, false>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp,
 									     false, pech_core{}, 0u, n))
 			   : il ? plan_il<COPY>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8)
 			   : COPY ? plan_step<COPY>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid)
 				  : plan_step<COPY, true>(cores, deltas, lds, npos, nlr, nrem, lane, g8, grp, grid, nspec, nppos);
-		if (!COPY && !FLAT) { // the descriptors where the step after N starts (flat: they are in LDS)
-			nppos = min(N.pos, nslots - 1u);
+		if (!COPY && (!FLAT || FLATG)) { // the descriptors where the step after N starts (flat: they are in LDS)
+			const uint32_t nlim = FLATG ? n : nslots;
+			nppos = min(N.pos, nlim - 1u);
 			if (jmax > 1u && N.rem == 0) {
 				// N ends a pooled item: the next item is the pending claim's
 				// (a guess: an item past its share's end moves on to the next
@@ -2491,9 +2507,12 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 				const uint32_t a = (uint32_t)(wg0 + (uint64_t)wg_rows * sh / PECH_MAIN_WAVES);
 				const uint32_t b = (uint32_t)(wg0 + (uint64_t)wg_rows * (sh + 1u) / PECH_MAIN_WAVES);
 				const uint32_t st = share_head(a, b) + (j - 1u) * PECH_ITEM_ROWS;
-				nppos = j < jmax && st < b ? min(st / U0, nslots - 1u) : nppos;
+				nppos = j < jmax && st < b ? min(st / U0, nlim - 1u) : nppos;
 			}
-			nspec = load_spec(cores, nppos + grp);
+			if constexpr (FLATG)
+				nspec_g = ((const u32x4 *)descs)[min(nppos + grp, n - 1u)];
+			else
+				nspec = load_spec(cores, nppos + grp);
 		}
 #else // A/B: N's descriptors loaded when N is planned
 		const Step N = FLAT ? (il ? plan_il<false, true>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8, lds)

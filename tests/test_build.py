@@ -111,6 +111,24 @@ def test_row_loops_never_drain_the_ring(device_asm, kernel):
         assert len(movs) <= 8, (name, len(movs))
 
 
+@pytest.mark.parametrize("kernel", ["pech_crc32c_main", "pech_crc32c_flat", "pech_crc32c_flatg", "pech_crc32c_direct"])
+def test_row_loops_keep_lookups_in_flight(device_asm, kernel):
+    """The hot row loop (the first block of Horner rows with prefetch loads)
+    waits for its LDS lookups with counted lgkmcnt, several in flight.  A
+    schedule that waits lgkmcnt(0) after every lookup pair ran flat launches
+    4-5 us slower: the runtime interleave decision in pech_crc32c_flat (v0.33
+    first build) and the scalar descriptor loads of flatg's small steps both
+    produced it (profiles/r06/ab_flat_il_fix.txt, flatg.txt)."""
+    asm, _ = device_asm
+    loops = [(n, ins) for n, ins, note in _blocks(kernel_body(asm, kernel))
+             if sum(i.startswith("v_perm_b32") for i in ins) >= 64
+             and sum(i.startswith("global_load_dwordx4") for i in ins) >= 4]
+    assert loops, kernel
+    name, ins = loops[0]
+    zero = sum("lgkmcnt(0)" in i for i in ins)
+    assert zero <= 16, (name, zero)
+
+
 def _loop_regions(body):
     """Every loop of a kernel body, from its "Loop Header" label to the last
     branch back to it (the fused-copy kernel's loops span several basic
