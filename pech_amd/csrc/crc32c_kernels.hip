@@ -3166,6 +3166,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.34 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) "(host:il),flatg<=" PECH_STR(PECH_FLATG_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.35 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) "(host:il),flatg<=" PECH_STR(PECH_FLATG_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }
