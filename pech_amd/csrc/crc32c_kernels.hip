@@ -664,6 +664,16 @@ __device__ __forceinline__ pech_core flatg_conv(u32x4 v, uint32_t p) // v: {addr
 	c.meta = p | (c.rows ? c.rows * PECH_ROW_BYTES - lb - len : 0u) << 20; // (T mod 2^32: exact, < 128)
 	return c;
 }
+// A descriptor loaded by a vector load and read only in part (flatg_conv
+// ignores the seed, the prologue the address's high word): its unread
+// registers were free for reuse while the load was in flight, and the
+// reuse waited for the load with a vmcnt(0) -- draining the tables' loads
+// at entry and the ring at a step's end.  Marking the whole vector read
+// where it is consumed keeps its registers until then.
+__device__ __forceinline__ void keep_whole(const u32x4 &v)
+{
+	asm volatile("" ::"v"(v));
+}
 __device__ __forceinline__ pech_core flatg_core(const pech_core *__restrict__ g, uint32_t p)
 {
 	return flatg_conv(((const u32x4 *)g)[uni(p)], p);
@@ -1677,6 +1687,7 @@ __device__ __forceinline__ bool prologue_flatg(uint32_t *lds, const u32x4 (&dv)[
 		rmin = p < n ? min(rmin, rows[k]) : rmin;
 		rmax = p < n ? max(rmax, rows[k]) : rmax;
 		sd = sd || (p < n && dv[k].w != 0u);
+		keep_whole(dv[k]);
 	}
 	const uint32_t incl = wave_incl_scan(tsum);
 	lds[L_FLAT / 4u + tid] = incl - tsum; // the thread's prefix inside its wave
@@ -2243,16 +2254,18 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		rem_all = wg_rows;
 	}
 	Step S;
-	if constexpr (FLATG)
+	if constexpr (FLATG) {
+		keep_whole(gspec);
 		S = plan_step<false, true, true, true>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false,
 						       flatg_conv(gspec, min(pg + grp, n - 1u)), pg, n);
-	else if constexpr (FLAT)
+	} else if constexpr (FLAT) {
 		S = il ? plan_il<false, true>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8, lds)
 		       : plan_step<false, false, true, false>(gdesc, deltas, lds, p0, lr0, rem_all, lane, g8, grp, false,
 							      pech_core{}, 0u, n);
-	else
+	} else {
 		S = il ? plan_il<COPY>(cores, deltas, p0, lr0, rem_all, wave * 8u + grp, g8)
 		       : plan_step<COPY, true>(cores, deltas, lds, p0, lr0, rem_all, lane, g8, grp, grid, spec, pg);
+	}
 	STAMP(t_plan);
 	uint32_t tpow = COPY ? 0u : rowpow(consts, S); // x^(8 128 ra) of the step's run (finish_run)
 	// Static shares walk on from where a step ends: the CRC kernel loads the
@@ -2488,6 +2501,8 @@ __device__ __forceinline__ void main_body(uint32_t *lds, const pech_core *__rest
 		// vector loads a step ahead; its scalar loads for the N of every
 		// step made the row loops' schedule serialise their LDS lookups,
 		// c4-64k 53.3 against 48.9 us for the planned main)
+		if constexpr (FLATG)
+			keep_whole(nspec_g);
 		const Step N = FLATG ? plan_step<false, true, true, true>(gdesc, deltas, lds, npos, nlr, nrem, lane, g8, grp, false,
 									 flatg_conv(nspec_g, min(nppos + grp, n - 1u)), nppos, n)
 			       : FLAT ? (il ? plan_il<false, true>(cores, deltas, npos, nlr, nrem, wave * 8u + grp, g8, lds)
@@ -3166,6 +3181,6 @@ extern "C" hipError_t pech_launch_direct(const pech_desc *descs, uint32_t n, con
 #define PECH_STR(x) PECH_STR2(x)
 extern "C" const char *pech_kernel_tag(void)
 {
-	return "pech_crc32c 0.35 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) "(host:il),flatg<=" PECH_STR(PECH_FLATG_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
+	return "pech_crc32c 0.36 gfx950 rows128 wave-steps(8x8-lane groups) prio-by-progress(static,pool-dry) split>=8rows small-deal<=4waves/wg,blocks32 grid-small-steps masked-heads flat<=" PECH_STR(PECH_FLAT_MAX) "(host:il),flatg<=" PECH_STR(PECH_FLATG_MAX) "(status-word) direct-small-batches(past-end-consts,wg-interleaved,copy) lds-bank-replicated-A128 mulmod-bitop3 rowpow next-spec(pool 2-ahead) early-fill<=" PECH_STR(PECH_EARLY_FILL_ROWS) "rows/wg U" PECH_STR(
 		PECH_U) " waves/CU " PECH_STR(PECH_MAIN_WAVES) " copy-blocks U" PECH_STR(PECH_U_COPY) " copy-il" PECH_STR(PECH_IL_COPY) " uniform-pool " PECH_STR(PECH_POOL_ROWS) "/" PECH_STR(PECH_ITEM_ROWS) " from " PECH_STR(PECH_POOL_MIN_SHARE);
 }
