@@ -652,9 +652,12 @@ __device__ __forceinline__ pech_core flat_core(const uint32_t *lds, uint32_t p)
 // Large flat batches (pech_crc32c_flatg, PECH_FLAT_MAX < n <= PECH_FLATG_MAX):
 // no LDS table -- 16 B per position would not fit beside the A_128 tables --
 // so a step's descriptors come from the caller's array itself (`g`: the
-// crc32c_desc array, L2-resident after the prologue read it), by SCALAR loads
-// at wave-uniform positions (lgkmcnt: the ring's vector loads are never
-// drained for them), each turned into the LDS table's {addr, rows, meta}.
+// crc32c_desc array, L2-resident after the prologue read it), each turned
+// into the LDS table's {addr, rows, meta}: a split step's one descriptor by a
+// scalar load at its wave-uniform position (lgkmcnt: the ring's vector loads
+// are never drained for it); a small-buffer step's eight, one per lane group,
+// from a vector prefetch issued a step ahead (plan_step's PRE), or on a miss
+// by a vector load (main_body).
 __device__ __forceinline__ pech_core flatg_conv(u32x4 v, uint32_t p) // v: {addr lo, addr hi, len, seed}
 {
 	pech_core c;
