@@ -181,8 +181,8 @@ def test_async_results_stored_by_the_kernel(monkeypatch, host_out):
     lone small batch is polled by the context's thread.  Lone payloads one at
     a time: 64 KiB and 1 MiB (flat), 4 KiB and 20 KiB pieces (direct), with
     and without seeds, a zero-length one; then slots of 300 x 40 KiB
-    (plan + main at the default flat limit; pech_crc32c_flatg, stored by the
-    kernel, at 4,096), then one of 4,200 pieces, one
+    (plan + main at a flat limit of 256; pech_crc32c_flatg, stored by the
+    kernel, at 4,096, the default), then one of 4,200 pieces, one
     of them 40 KiB (plan + main, results copied)."""
     import pech_amd as P
 
@@ -207,8 +207,8 @@ def test_async_results_stored_by_the_kernel(monkeypatch, host_out):
     assert lone >= 3 * (len(sizes) - 1), st
     assert st["polled"] == lone, st  # every lone batch of <= 8 MiB polled
     assert st["host_out"] == (lone if host_out == "1" else 0), st
-    # 300 pieces in one slot: plan + main at the default flat limit (256),
-    # pech_crc32c_flatg with results stored by the kernel at 4,096
+    # 300 pieces in one slot: plan + main at a flat limit of 256,
+    # pech_crc32c_flatg with results stored by the kernel at 4,096 (the default)
     base = dict(got)
     prev = P.set_flat_max(256)
     try:
